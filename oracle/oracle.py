@@ -1,0 +1,175 @@
+"""ctypes binding of oracle/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+The CPU restatement of the reference path (see trik_oracle.h for what it
+restates and its parity status).  Only tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg may import this module; the product package
+(trik-media-sensors-dsp_amd/trik_hsv) must never import it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+LAYOUT_YUYV = 0
+LAYOUT_OV7670 = 1
+
+
+class Range(C.Structure):
+    """Mirrors TRIK_VIDTRANSCODE_CV_InArgsAlg's HSV fields
+    (trik/webcam/object_sensor/trik_vidtranscode_cv.h:48-56)."""
+
+    _fields_ = [
+        ("hue_from", C.c_uint16),
+        ("hue_to", C.c_uint16),
+        ("sat_from", C.c_uint8),
+        ("sat_to", C.c_uint8),
+        ("val_from", C.c_uint8),
+        ("val_to", C.c_uint8),
+    ]
+
+
+def build() -> str:
+    """Compile liboracle.so in place (gcc) and return its path."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        u32, i32, i64, u64 = C.c_uint32, C.c_int32, C.c_int64, C.c_uint64
+        vp = C.c_void_p
+        for name in ("add2", "packh2", "packlh2", "pack2", "packhl2", "maxu4", "minu4",
+                     "cmpeq2", "packh4", "cmpltu4", "cmpgtu4", "spacku4"):
+            f = getattr(L, "trik_c64x_" + name)
+            f.argtypes, f.restype = [u32, u32], u32
+        for name in ("unpkhu4", "unpklu4", "swap4"):
+            f = getattr(L, "trik_c64x_" + name)
+            f.argtypes, f.restype = [u32], u32
+        L.trik_c64x_mpyu4ll.argtypes, L.trik_c64x_mpyu4ll.restype = [u32, u32], u64
+        L.trik_c64x_dotpus4.argtypes, L.trik_c64x_dotpus4.restype = [u32, u32], i32
+        L.trik_c64x_dotpn2.argtypes, L.trik_c64x_dotpn2.restype = [u32, u32], i32
+        L.trik_c64x_shr2.argtypes, L.trik_c64x_shr2.restype = [u32, u32], u32
+        L.trik_c64x_clr.argtypes, L.trik_c64x_clr.restype = [u32, u32, u32], u32
+        L.trik_oracle_luts.argtypes, L.trik_oracle_luts.restype = [vp, vp], None
+        L.trik_oracle_pair_rgb_c64x.argtypes, L.trik_oracle_pair_rgb_c64x.restype = [u32, vp], None
+        L.trik_oracle_hsv_c64x.argtypes, L.trik_oracle_hsv_c64x.restype = [u32], u32
+        L.trik_oracle_rgb_closed.argtypes, L.trik_oracle_rgb_closed.restype = [u32, u32, u32], u32
+        L.trik_oracle_hsv_closed.argtypes, L.trik_oracle_hsv_closed.restype = [u32], u32
+        L.trik_oracle_pack_range.argtypes = [C.POINTER(Range), vp, vp, vp]
+        L.trik_oracle_pack_range.restype = None
+        L.trik_oracle_detect.argtypes, L.trik_oracle_detect.restype = [u32, u32, u32, u32], C.c_int
+        L.trik_oracle_yuv_table.argtypes, L.trik_oracle_yuv_table.restype = [vp, C.c_int], None
+        L.trik_oracle_frame.argtypes = [vp, i64, C.c_int, C.c_int, C.c_int, C.c_int,
+                                        vp, C.c_int, vp, vp]
+        L.trik_oracle_frame.restype = C.c_int
+        L.trik_oracle_targets.argtypes = [vp, C.c_int, C.c_int, vp, vp, vp]
+        L.trik_oracle_targets.restype = None
+        L.trik_oracle_batch.argtypes = [vp, i64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                        vp, C.c_int, vp, vp, C.c_int]
+        L.trik_oracle_batch.restype = C.c_int
+        L.trik_oracle_synth.argtypes = [vp, i64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                        C.c_int, C.c_int, u64]
+        L.trik_oracle_synth.restype = None
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def ranges_array(ranges) -> C.Array:
+    """ranges: iterable of (hue_from, hue_to, sat_from, sat_to, val_from, val_to)."""
+    rs = list(ranges)
+    arr = (Range * max(1, len(rs)))()
+    for i, r in enumerate(rs):
+        arr[i] = Range(*r)
+    return arr
+
+
+def luts():
+    a, b = np.zeros(256, np.uint16), np.zeros(256, np.uint16)
+    lib().trik_oracle_luts(_ptr(a), _ptr(b))
+    return a, b
+
+
+def pair_rgb(yuyv: int):
+    out = np.zeros(2, np.uint32)
+    lib().trik_oracle_pair_rgb_c64x(yuyv, _ptr(out))
+    return int(out[0]), int(out[1])
+
+
+def yuv_table(closed: bool) -> np.ndarray:
+    """(rgb << 32 | hsv) for every (Y,U,V); index = Y | U<<8 | V<<16."""
+    out = np.zeros(1 << 24, np.uint64)
+    lib().trik_oracle_yuv_table(_ptr(out), 1 if closed else 0)
+    return out
+
+
+def pack_range(r):
+    f, t, e = C.c_uint32(), C.c_uint32(), C.c_uint32()
+    lib().trik_oracle_pack_range(C.byref(Range(*r)), C.byref(f), C.byref(t), C.byref(e))
+    return f.value, t.value, e.value
+
+
+def frame_bytes(width, height, line_length, layout) -> int:
+    return height * line_length * (2 if layout == LAYOUT_OV7670 else 1)
+
+
+def frame(frame_u8: np.ndarray, width, height, line_length, layout, ranges, want_mask=False):
+    """Run one frame; returns (sums[T,3] int64, mask[H,W] uint8 or None)."""
+    rs = list(ranges)
+    sums = np.zeros((max(1, len(rs)), 3), np.int64)
+    mask = np.zeros((height, width), np.uint8) if want_mask else None
+    fr = np.ascontiguousarray(frame_u8, dtype=np.uint8)
+    rc = lib().trik_oracle_frame(_ptr(fr), fr.size, width, height, line_length, layout,
+                                 ranges_array(rs), len(rs), _ptr(sums),
+                                 _ptr(mask) if want_mask else None)
+    if rc != 0:
+        raise ValueError("oracle rejected frame (reference setup/run would fail)")
+    return sums[: len(rs)], mask
+
+
+def targets(sums3, width, height):
+    s = np.ascontiguousarray(np.asarray(sums3, np.int64))
+    x, y, z = C.c_int8(), C.c_int8(), C.c_uint8()
+    lib().trik_oracle_targets(_ptr(s), width, height, C.byref(x), C.byref(y), C.byref(z))
+    return x.value, y.value, z.value
+
+
+def batch(frames_u8: np.ndarray, frame_stride, n_frames, width, height, line_length, layout,
+          ranges, n_threads=1):
+    """Returns (sums[N,T,3] int64, targets[N,T,3] int8 (x, y, size as int8 bits))."""
+    rs = list(ranges)
+    T = len(rs)
+    sums = np.zeros((n_frames, T, 3), np.int64)
+    tg = np.zeros((n_frames, T, 3), np.int8)
+    rc = lib().trik_oracle_batch(_ptr(frames_u8), frame_stride, n_frames, width, height,
+                                 line_length, layout, ranges_array(rs), T, _ptr(sums), _ptr(tg),
+                                 n_threads)
+    if rc != 0:
+        raise ValueError("oracle rejected batch")
+    return sums, tg
+
+
+def synth(n_frames, width, height, line_length, layout, kind, seed, first_frame=0,
+          frame_stride=None) -> np.ndarray:
+    fb = frame_bytes(width, height, line_length, layout)
+    stride = fb if frame_stride is None else frame_stride
+    out = np.zeros(stride * n_frames, np.uint8)
+    lib().trik_oracle_synth(_ptr(out), stride, first_frame, n_frames, width, height,
+                            line_length, layout, kind, seed)
+    return out

@@ -1,0 +1,127 @@
+/*
+ * trik_oracle.h -- CPU restatement of the TRIK HSV-threshold + centroid path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the parity checker for the MI355X HIP
+ * path in trik-media-sensors-dsp_amd/.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it.  The product library
+ * (libtrik_hsv.so) never links or calls it.
+ *
+ * What it restates (paths relative to the reference checkout):
+ *   trik/webcam/object_sensor/include/internal/cv_ball_detector_seqpass.hpp
+ *     (alias WSEQ)  -- the active webcam object-sensor implementation
+ *   trik/ov7670/object_sensor/include/internal/cv_ball_detector_seqpass.hpp
+ *     (alias OSEQ)  -- the ov7670 semi-planar input layout (OSEQ:343-387)
+ *
+ * Two independent derivations of the per-pixel arithmetic live here:
+ *   1. an intrinsic-level restatement that follows WSEQ:181-249 step by step
+ *      over a C emulation of the TI C64x+ intrinsics it uses (semantics from
+ *      TI's published C64x+ intrinsic definitions);
+ *   2. a closed-form restatement.
+ * tests/test_oracle.py requires them to agree on all 2^24 inputs.
+ *
+ * PARITY STATUS: the reference ships no tests, fixtures or golden vectors,
+ * and its hot path cannot be compiled here (it needs TI's <c6x.h> and the
+ * XDAIS headers, which are absent; building it with stand-in headers is not
+ * allowed).  Parity is therefore "unpinned" by reference artefacts.  It is
+ * pinned instead by the two derivations above, per-intrinsic unit tests and
+ * the SURVEY Appendix A known-answer table.  See DESIGN.md section 3.
+ */
+#ifndef TRIK_ORACLE_H_
+#define TRIK_ORACLE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  TRIK_ORACLE_LAYOUT_YUYV   = 0, /* packed Y0 U Y1 V (webcam, WSEQ:251-284) */
+  TRIK_ORACLE_LAYOUT_OV7670 = 1  /* Y plane + chroma plane (OSEQ:343-387) */
+};
+
+/* Mirrors TRIK_VIDTRANSCODE_CV_InArgsAlg (webcam trik_vidtranscode_cv.h:48-56). */
+typedef struct trik_oracle_range {
+  uint16_t hue_from, hue_to; /* 0..359 */
+  uint8_t sat_from, sat_to;  /* 0..100 */
+  uint8_t val_from, val_to;  /* 0..100 */
+} trik_oracle_range;
+
+/* --- C64x+ intrinsic emulation (exported for the per-intrinsic unit tests) --- */
+uint64_t trik_c64x_mpyu4ll(uint32_t a, uint32_t b);
+int32_t  trik_c64x_dotpus4(uint32_t a, uint32_t b);
+uint32_t trik_c64x_add2(uint32_t a, uint32_t b);
+uint32_t trik_c64x_packh2(uint32_t a, uint32_t b);
+uint32_t trik_c64x_packlh2(uint32_t a, uint32_t b);
+uint32_t trik_c64x_pack2(uint32_t a, uint32_t b);
+uint32_t trik_c64x_packhl2(uint32_t a, uint32_t b);
+uint32_t trik_c64x_shr2(uint32_t a, uint32_t n);
+uint32_t trik_c64x_clr(uint32_t a, uint32_t lo, uint32_t hi);
+uint32_t trik_c64x_spacku4(uint32_t a, uint32_t b);
+uint32_t trik_c64x_unpkhu4(uint32_t a);
+uint32_t trik_c64x_unpklu4(uint32_t a);
+uint32_t trik_c64x_maxu4(uint32_t a, uint32_t b);
+uint32_t trik_c64x_minu4(uint32_t a, uint32_t b);
+uint32_t trik_c64x_cmpeq2(uint32_t a, uint32_t b);
+int32_t  trik_c64x_dotpn2(uint32_t a, uint32_t b);
+uint32_t trik_c64x_packh4(uint32_t a, uint32_t b);
+uint32_t trik_c64x_cmpltu4(uint32_t a, uint32_t b);
+uint32_t trik_c64x_cmpgtu4(uint32_t a, uint32_t b);
+uint32_t trik_c64x_swap4(uint32_t a);
+
+/* --- per-pixel arithmetic --- */
+/* s_mult43_div / s_mult255_div, WSEQ:389-407. */
+void     trik_oracle_luts(uint16_t lut43[256], uint16_t lut255[256]);
+/* WSEQ:181-205: one YUYV word (b0=Y0,b1=U,b2=Y1,b3=V) -> two 0x00RRGGBB words. */
+void     trik_oracle_pair_rgb_c64x(uint32_t yuyv, uint32_t rgb_out[2]);
+/* WSEQ:207-249: 0x00RRGGBB -> 0x00VVSSHH. */
+uint32_t trik_oracle_hsv_c64x(uint32_t rgb888);
+/* SURVEY Appendix A closed forms of the same two stages. */
+uint32_t trik_oracle_rgb_closed(uint32_t y, uint32_t u, uint32_t v);
+uint32_t trik_oracle_hsv_closed(uint32_t rgb888);
+
+/* WSEQ:425-445: InArgs -> packed (from, to, expect) words. */
+void     trik_oracle_pack_range(const trik_oracle_range* r, uint32_t* from,
+                                uint32_t* to, uint32_t* expect);
+/* WSEQ:171-179. */
+int      trik_oracle_detect(uint32_t hsv, uint32_t from, uint32_t to, uint32_t expect);
+
+/* Table of (rgb<<32 | hsv) for every (Y,U,V): index = Y | U<<8 | V<<16.
+ * closed != 0 selects the closed-form derivation. out has 2^24 entries. */
+void     trik_oracle_yuv_table(uint64_t* out, int closed);
+
+/* One frame through WSEQ:412-508 (or the OSEQ layout) for T ranges.
+ * sums[3*t + {0,1,2}] = {targetPoints, targetX sum, targetY sum} as the
+ * reference accumulates them (WSEQ:316-354).  mask (optional, W*H bytes)
+ * receives the per-pixel T-bit detection mask (bit t = range t).
+ * Returns 0, or -1 where the reference's setup/run would fail
+ * (W%32, H%4, negative dims: WSEQ:365-369; H*lineLength > size: WSEQ:415). */
+int      trik_oracle_frame(const uint8_t* frame, int64_t frame_size, int width,
+                           int height, int line_length, int layout,
+                           const trik_oracle_range* ranges, int n_ranges,
+                           int64_t* sums, uint8_t* mask);
+
+/* WSEQ:486-505 epilogue: sums {N, sumX, sumY} -> targetX/Y/Size. */
+void     trik_oracle_targets(const int64_t sums[3], int width, int height,
+                             int8_t* target_x, int8_t* target_y, uint8_t* target_size);
+
+/* Batch of frames split over n_threads POSIX threads (the CPU baseline).
+ * sums is [n_frames][n_ranges][3]; targets is [n_frames][n_ranges][3] bytes
+ * (x, y, size) and may be NULL. */
+int      trik_oracle_batch(const uint8_t* frames, int64_t frame_stride, int n_frames,
+                           int width, int height, int line_length, int layout,
+                           const trik_oracle_range* ranges, int n_ranges,
+                           int64_t* sums, int8_t* targets, int n_threads);
+
+/* Synthetic frame generators shared bit-for-bit with the device generator
+ * (trik-media-sensors-dsp_amd/csrc/trik_hsv_synth.hip).
+ * kind 0 = uniform random bytes, kind 1 = scene (gradients + 6 discs). */
+void     trik_oracle_synth(uint8_t* frames, int64_t frame_stride, int first_frame,
+                           int n_frames, int width, int height, int line_length,
+                           int layout, int kind, uint64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TRIK_ORACLE_H_ */

@@ -1,0 +1,89 @@
+"""Generate tests/golden/oracle_golden.json from the CPU oracle.
+
+Run from the repo root:  python tests/golden/make_golden.py
+
+What the fixture holds (inputs are regenerated from seeds, not stored):
+  * sha256 of the 2^24-entry per-(Y,U,V) table of (rgb << 32 | hsv), both
+    derivations (they must be identical), plus 4096 sampled entries;
+  * frame cases: (W, H, lineLength, layout, generator kind, seed, ranges) with
+    the sha256 of the generated frame bytes (pins the generator) and the
+    expected per-range {N, sumX, sumY} and {targetX, targetY, targetSize}.
+
+These vectors are produced by the repo's own restatement of the reference
+(the reference ships none and cannot be built here -- DESIGN.md section 3),
+so they pin regressions and the GPU path, not the reference itself.
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
+import oracle as O  # noqa: E402
+
+# BASELINE ranges T0..T3 plus edge cases
+RANGES = {
+    "T0": (0, 30, 50, 100, 30, 100),
+    "T1": (90, 150, 40, 100, 20, 100),
+    "T2": (200, 260, 40, 100, 20, 100),
+    "T3_wrap": (330, 20, 30, 100, 30, 100),
+    "full": (0, 359, 0, 100, 0, 100),
+    "empty_point": (10, 10, 100, 100, 100, 100),
+    "from_eq_to": (120, 120, 0, 100, 0, 100),
+    "wrap_adjacent": (2, 1, 0, 100, 0, 100),
+    "wrap_359_0": (359, 0, 20, 100, 20, 100),
+    "clamped_args": (400, 500, 200, 250, 0, 255),
+    "grey": (0, 359, 0, 0, 0, 100),
+    "dark": (0, 359, 0, 100, 0, 10),
+}
+
+CASES = [
+    # name, W, H, lineLength, layout, kind, seed, frame, range names
+    ("c1_ov7670_320x240_uniform", 320, 240, 320, O.LAYOUT_OV7670, 0, 0x7A1C, 0, ["T0"]),
+    ("c1_ov7670_320x240_scene", 320, 240, 320, O.LAYOUT_OV7670, 1, 0x7A1C, 3, ["T0", "T1", "T2", "T3_wrap"]),
+    ("c2_yuyv_640x480_uniform", 640, 480, 1280, O.LAYOUT_YUYV, 0, 0x7A1C, 0, ["T0"]),
+    ("c2_yuyv_640x480_scene", 640, 480, 1280, O.LAYOUT_YUYV, 1, 0x7A1C, 1, list(RANGES)),
+    ("c3_yuyv_640x480_frame4095", 640, 480, 1280, O.LAYOUT_YUYV, 0, 0x7A1C, 4095, ["T0", "T1", "T2", "T3_wrap"]),
+    ("c4_yuyv_1280x720_scene", 1280, 720, 2560, O.LAYOUT_YUYV, 1, 0x7A1C, 7, ["T0", "T1"]),
+    ("ragged_linelength_64x8", 64, 8, 160, O.LAYOUT_YUYV, 0, 99, 0, list(RANGES)),
+    ("ragged_ov7670_96x12", 96, 12, 112, O.LAYOUT_OV7670, 0, 5, 2, list(RANGES)),
+    ("minimal_32x4", 32, 4, 64, O.LAYOUT_YUYV, 0, 1, 0, list(RANGES)),
+    ("empty_frame_640x0", 640, 0, 1280, O.LAYOUT_YUYV, 0, 1, 0, ["T0", "full"]),
+]
+
+
+def main():
+    out = {"generator": "tests/golden/make_golden.py", "ranges": RANGES}
+    a = O.yuv_table(closed=False)
+    b = O.yuv_table(closed=True)
+    assert np.array_equal(a, b), "derivations disagree"
+    out["yuv_table_sha256"] = hashlib.sha256(a.tobytes()).hexdigest()
+    rng = np.random.default_rng(20261015)
+    idx = rng.integers(0, 1 << 24, 4096)
+    out["yuv_table_samples"] = [[int(i), int(a[i])] for i in idx]
+    lut43, lut255 = O.luts()
+    out["lut43"] = lut43.tolist()
+    out["lut255"] = lut255.tolist()
+    out["packed_ranges"] = {k: list(O.pack_range(v)) for k, v in RANGES.items()}
+    cases = []
+    for name, w, h, ll, layout, kind, seed, fidx, rnames in CASES:
+        fr = O.synth(1, w, h, ll, layout, kind, seed, first_frame=fidx)
+        sums, _ = O.frame(fr, w, h, ll, layout, [RANGES[r] for r in rnames])
+        tg = [list(O.targets(s, w, h)) for s in sums]
+        cases.append({
+            "name": name, "width": w, "height": h, "line_length": ll, "layout": layout,
+            "kind": kind, "seed": seed, "frame": fidx, "ranges": rnames,
+            "frame_sha256": hashlib.sha256(fr.tobytes()).hexdigest(),
+            "sums": sums.tolist(), "targets": tg,
+        })
+    out["cases"] = cases
+    with open(os.path.join(HERE, "oracle_golden.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print("wrote", len(cases), "cases")
+
+
+if __name__ == "__main__":
+    main()
