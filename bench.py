@@ -1,0 +1,183 @@
+"""Benchmark: HSV-threshold + centroid on batches of 640x480 YUYV frames.
+
+Workload (BASELINE.json configs[2], "C3"): 4096 frames x 640x480 packed YUYV
+per GPU, 4 HSV target ranges, frames synthesised on the device (SplitMix64
+uniform bytes) before the timed region, so inputs are resident in HBM.  A
+step = one full pass of the hot path over the batch: zero the per-frame sums,
+the fused detect + reduce kernel, the target epilogue kernel, and the
+per-target batch totals (RCCL all-reduce across GPUs when N > 1).
+
+With N GPUs (torch.distributed.run, one process per GPU) each rank owns its
+own 4096 frames (global frames rank*4096 ...): weak scaling; at N = 8 this is
+BASELINE configs[4] (32768 frames over 8 GPUs).
+
+Prints one JSON line (rank 0).  `roofline` is measured live with HIP events
+around the hot kernel on the stream it is launched on; `cpu_baseline` times
+the repo's CPU oracle (oracle/, test infrastructure) on a bounded sample of
+the same frames on this host's cores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "trik-media-sensors-dsp_amd"))
+
+METRIC = "Mpixels/sec HSV-threshold+centroid on 640×480 YUYV batches; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+RANGES = [(0, 30, 50, 100, 30, 100), (90, 150, 40, 100, 20, 100),
+          (200, 260, 40, 100, 20, 100), (330, 20, 30, 100, 30, 100)]
+SEED = 0x7A1C
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=4096, help="frames per GPU")
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--targets", type=int, default=4)
+    ap.add_argument("--kind", type=int, default=0, help="0 uniform random bytes, 1 scene")
+    ap.add_argument("--cpu-frames", type=int, default=512, help="CPU baseline sample (frames)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
+                    help="rocprofv3 FETCH_SIZE summary used for roofline.traffic")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, width, height, ll, n_ranges, gpu_sums):
+    """Oracle (CPU port of the reference path) on a bounded sample; parity on it too."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    cores = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail)), 64))
+    n = min(args.cpu_frames, args.frames)
+    host = oracle.synth(n, width, height, ll, oracle.LAYOUT_YUYV, args.kind, SEED)
+    t0 = time.perf_counter()
+    sums, _ = oracle.batch(host, height * ll, n, width, height, ll, oracle.LAYOUT_YUYV,
+                           RANGES[:n_ranges], n_threads=cores)
+    dt = time.perf_counter() - t0
+    parity = bool(np.array_equal(sums, gpu_sums[:n]))
+    return {"value": round(n * width * height / dt / 1e6, 3), "unit": "Mpix/s", "cores": cores,
+            "kind": "port",
+            "sample": f"{n} frames x {width}x{height} YUYV, {n_ranges} ranges "
+                      f"(frames 0..{n - 1} of the GPU batch), {cores} threads, {dt:.2f} s"}, parity
+
+
+def load_traffic(path, bytes_per_launch):
+    try:
+        with open(path) as f:
+            pmc = json.load(f)
+        if pmc.get("bytes_per_launch_algorithmic") == bytes_per_launch:
+            return pmc.get("hbm_read_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import trik_hsv
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    W, H, F, T = args.width, args.height, args.frames, args.targets
+    ll = 2 * W
+    fb = H * ll
+    ranges = RANGES[:T]
+    frames = torch.empty(F * fb, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream()
+    trik_hsv.synth(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, args.kind, SEED, first_frame=rank * F)
+    det = trik_hsv.Detector()
+    sums = torch.zeros((F, T, 3), dtype=torch.int64, device=dev)
+    totals = torch.zeros((T, 3), dtype=torch.int64, device=dev)
+
+    def step(ev0=None, ev1=None):
+        sums.zero_()
+        if ev0 is not None:
+            ev0.record(stream)
+        det.batch_sums(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, ranges, sums, stream=stream)
+        if ev1 is not None:
+            ev1.record(stream)
+        targets = trik_hsv.batch_targets(sums, W, H, stream=stream)
+        torch.sum(sums, dim=0, out=totals)
+        if world > 1:
+            dist.all_reduce(totals)  # RCCL over xGMI: 3*T int64 per step
+        return targets
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(*evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+
+    el = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms_max = float(el[0]), float(el[1])
+
+    px_total = world * F * W * H * args.steps
+    value = px_total / elapsed / 1e6
+    bytes_per_launch = F * fb  # algorithmic: 2 B/pixel read once
+    achieved = bytes_per_launch / (kern_ms / 1e3) / 1e9
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "Mpix/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: device SplitMix64 uniform bytes, seed 0x7A1C" if args.kind == 0
+                else "synthetic: device scene generator (gradients + 6 discs), seed 0x7A1C",
+        "config": {"workload": f"C3: batch {F} x {W}x{H} YUYV per GPU, {T} HSV targets"
+                               + (f" (C5 at N=8: {F * world} frames)" if world > 1 else ""),
+                   "frames_per_gpu": F, "width": W, "height": H, "line_length": ll,
+                   "targets": T, "layout": "yuyv", "parallelism": f"dp{world} (frame shards)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": load_traffic(args.pmc, bytes_per_launch),
+                     "kernel": "reduce_kernel<YUYV,4>", "kernel_ms": round(kern_ms, 4),
+                     "kernel_ms_max_rank": round(kern_ms_max, 4),
+                     "bytes_per_launch": bytes_per_launch},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb, parity = cpu_baseline(args, W, H, ll, T, sums.cpu().numpy())
+        out["cpu_baseline"] = cb
+        out["cpu_sample_parity"] = parity
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    det.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,344 @@
+/*
+ * trik_hsv.h -- C ABI of the MI355X-native TRIK HSV-threshold + centroid path.
+ *
+ * Drop-in boundary for the reference's object-sensor codec.  All paths below
+ * are relative to the reference checkout (trikset/trik-media-sensors-dsp):
+ *   WPUB   trik/webcam/object_sensor/trik_vidtranscode_cv.h
+ *   OPUB   trik/ov7670/object_sensor/trik_vidtranscode_cv.h
+ *   WFXNS  trik/webcam/object_sensor/src/vidtranscode_cv_fxns.c
+ *   WGLUE  trik/webcam/object_sensor/src/vidtranscode_cv.cpp
+ *   WINT   trik/webcam/object_sensor/include/internal/vidtranscode_cv.h
+ *   WSEQ   trik/webcam/object_sensor/include/internal/cv_ball_detector_seqpass.hpp
+ *
+ * Two layers:
+ *  1. The XDAIS-shaped quartet create / control / process / delete.  It keeps
+ *     the reference's struct field order, argument meaning and return codes
+ *     (TI's xdas.h / ialg.h / xdm.h / ividtranscode.h are not in this image,
+ *     so the base structs are restated here with 32-bit XDAS_Int32 fields;
+ *     sizes are this ABI's, documented in INTEGRATION.md).  process() takes a
+ *     host frame, like the reference's ARM->DSP call.
+ *  2. A batched device API (trik_hsv_*) that the quartet sits on: N frames
+ *     resident in HBM, T HSV ranges, per-frame per-range results.  This is
+ *     where the HIP kernels run.
+ *
+ * No torch or HIP types cross this ABI: device buffers and streams are plain
+ * pointers (a hipStream_t passed as void*; NULL = the null stream).
+ * Errors are return codes; no C++ exception crosses it.
+ */
+#ifndef TRIK_HSV_H_
+#define TRIK_HSV_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------------- */
+/* Return codes and XDM constants (TI ialg.h / xdm.h values)               */
+/* ---------------------------------------------------------------------- */
+#define TRIK_IALG_EOK 0                   /* IALG_EOK */
+#define TRIK_IALG_EFAIL (-1)              /* IALG_EFAIL */
+#define TRIK_IVIDTRANSCODE_EOK 0          /* IVIDTRANSCODE_EOK */
+#define TRIK_IVIDTRANSCODE_EFAIL (-1)     /* IVIDTRANSCODE_EFAIL */
+#define TRIK_IVIDTRANSCODE_EUNSUPPORTED (-3) /* IVIDTRANSCODE_EUNSUPPORTED */
+
+/* XDM_CmdId (control commands used at WFXNS:285-330) */
+#define TRIK_XDM_GETSTATUS 0
+#define TRIK_XDM_SETPARAMS 1
+#define TRIK_XDM_RESET 2
+#define TRIK_XDM_SETDEFAULT 3
+#define TRIK_XDM_FLUSH 4
+#define TRIK_XDM_GETBUFINFO 5
+#define TRIK_XDM_GETVERSION 6
+
+/* extendedError bits set by XDM_SETUNSUPPORTEDPARAM / XDM_SETCORRUPTEDDATA */
+#define TRIK_XDM_CORRUPTEDDATA_BIT 11
+#define TRIK_XDM_UNSUPPORTEDPARAM_BIT 14
+/* accessMask bits (XDM_SETACCESSMODE_READ / _WRITE) */
+#define TRIK_XDM_ACCESSMODE_READ 0
+#define TRIK_XDM_ACCESSMODE_WRITE 1
+
+#define TRIK_XDM_CUSTOMENUMBASE 0x100     /* XDM_CUSTOMENUMBASE (TI xdm.h) */
+#define TRIK_IVIDTRANSCODE_MAXOUTSTREAMS 2
+#define TRIK_XDM_MAX_IO_BUFFERS 16
+
+/* TRIK_VIDTRANSCODE_CV_VideoFormat, WPUB:21-29 and OPUB:21-32 */
+typedef enum TRIK_VIDTRANSCODE_CV_VideoFormat {
+  TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_UNKNOWN = 0,
+  TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_RGB888 = TRIK_XDM_CUSTOMENUMBASE,
+  TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_RGB565,
+  TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_RGB565X,
+  TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_YUV444,
+  TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_YUV422,  /* packed YUYV (webcam) */
+  TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_YUV422P  /* Y plane + chroma plane (ov7670) */
+} TRIK_VIDTRANSCODE_CV_VideoFormat;
+
+/* ---------------------------------------------------------------------- */
+/* XDAIS-mirror structs                                                    */
+/* ---------------------------------------------------------------------- */
+
+/* IVIDTRANSCODE_Params, field order from the initialiser at WGLUE:153-184. */
+typedef struct TRIK_IVIDTRANSCODE_Params {
+  int32_t size;
+  int32_t numOutputStreams;
+  int32_t formatInput;
+  int32_t formatOutput[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t maxHeightInput;
+  int32_t maxWidthInput;
+  int32_t maxFrameRateInput;
+  int32_t maxBitRateInput;
+  int32_t maxHeightOutput[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t maxWidthOutput[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t maxFrameRateOutput[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t maxBitRateOutput[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t dataEndianness;
+} TRIK_IVIDTRANSCODE_Params;
+
+/* TRIK_VIDTRANSCODE_CV_Params, WPUB:32-34 */
+typedef struct TRIK_VIDTRANSCODE_CV_Params {
+  TRIK_IVIDTRANSCODE_Params base;
+} TRIK_VIDTRANSCODE_CV_Params;
+
+/* IVIDTRANSCODE_DynamicParams, field order from WGLUE:205-258. */
+typedef struct TRIK_IVIDTRANSCODE_DynamicParams {
+  int32_t size;
+  int32_t readHeaderOnlyFlag;
+  int32_t keepInputResolutionFlag[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t outputHeight[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t outputWidth[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t keepInputFrameRateFlag[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t inputFrameRate;
+  int32_t outputFrameRate[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t targetBitRate[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t rateControl[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t keepInputGOPFlag[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t intraFrameInterval[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t interFrameInterval[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t forceFrame[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t frameSkipTranscodeFlag[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+} TRIK_IVIDTRANSCODE_DynamicParams;
+
+/* TRIK_VIDTRANSCODE_CV_DynamicParams, WPUB:37-45 */
+typedef struct TRIK_VIDTRANSCODE_CV_DynamicParams {
+  TRIK_IVIDTRANSCODE_DynamicParams base;
+  int32_t inputHeight;
+  int32_t inputWidth;
+  int32_t inputLineLength;
+  int32_t outputLineLength[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+} TRIK_VIDTRANSCODE_CV_DynamicParams;
+
+/* TRIK_VIDTRANSCODE_CV_InArgsAlg, WPUB:48-56 (XDAS_Bool restated as int32) */
+typedef struct TRIK_VIDTRANSCODE_CV_InArgsAlg {
+  uint16_t detectHueFrom; /* [0..359] */
+  uint16_t detectHueTo;   /* [0..359]; From > To wraps through 0 (WSEQ:439-445) */
+  uint8_t detectSatFrom;  /* [0..100] */
+  uint8_t detectSatTo;
+  uint8_t detectValFrom;  /* [0..100] */
+  uint8_t detectValTo;
+  int32_t autoDetectHsv;  /* not implemented: see INTEGRATION.md */
+} TRIK_VIDTRANSCODE_CV_InArgsAlg;
+
+/* IVIDTRANSCODE_InArgs base fields used at WFXNS:192-224 */
+typedef struct TRIK_IVIDTRANSCODE_InArgs {
+  int32_t size;
+  int32_t numBytes;
+  int32_t inputID;
+} TRIK_IVIDTRANSCODE_InArgs;
+
+typedef struct TRIK_VIDTRANSCODE_CV_InArgs { /* WPUB:58-61 */
+  TRIK_IVIDTRANSCODE_InArgs base;
+  TRIK_VIDTRANSCODE_CV_InArgsAlg alg;
+} TRIK_VIDTRANSCODE_CV_InArgs;
+
+/* TRIK_VIDTRANSCODE_CV_OutArgsAlg, WPUB:64-74 */
+typedef struct TRIK_VIDTRANSCODE_CV_OutArgsAlg {
+  int8_t targetX;    /* [-100..100] */
+  int8_t targetY;    /* [-100..100] */
+  uint8_t targetSize; /* [0..100] */
+  uint16_t detectHue;
+  uint16_t detectHueTolerance;
+  uint16_t detectSat;
+  uint16_t detectSatTolerance;
+  uint16_t detectVal;
+  uint16_t detectValTolerance;
+} TRIK_VIDTRANSCODE_CV_OutArgsAlg;
+
+/* XDM1_SingleBufDesc */
+typedef struct TRIK_XDM1_SingleBufDesc {
+  int8_t* buf;
+  int32_t bufSize;
+  int32_t accessMask;
+} TRIK_XDM1_SingleBufDesc;
+
+/* XDM1_BufDesc (process input, WFXNS:199-214) */
+typedef struct TRIK_XDM1_BufDesc {
+  int32_t numBufs;
+  TRIK_XDM1_SingleBufDesc descs[TRIK_XDM_MAX_IO_BUFFERS];
+} TRIK_XDM1_BufDesc;
+
+/* XDM_BufDesc (process output, WFXNS:200,228-230) */
+typedef struct TRIK_XDM_BufDesc {
+  int8_t** bufs;
+  int32_t numBufs;
+  int32_t* bufSizes;
+} TRIK_XDM_BufDesc;
+
+/* IVIDTRANSCODE_OutArgs base fields written at WFXNS:195-261 */
+typedef struct TRIK_IVIDTRANSCODE_OutArgs {
+  int32_t size;
+  int32_t extendedError;
+  int32_t bitsConsumed;
+  int32_t decodedPictureType;
+  int32_t decodedPictureStructure;
+  int32_t decodedHeight;
+  int32_t decodedWidth;
+  TRIK_XDM1_SingleBufDesc encodedBuf[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t bitsGenerated[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t encodedPictureType[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t encodedPictureStructure[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t outputID[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t inputFrameSkipTranscodeFlag[TRIK_IVIDTRANSCODE_MAXOUTSTREAMS];
+  int32_t outBufsInUseFlag;
+} TRIK_IVIDTRANSCODE_OutArgs;
+
+typedef struct TRIK_VIDTRANSCODE_CV_OutArgs { /* WPUB:76-79 */
+  TRIK_IVIDTRANSCODE_OutArgs base;
+  TRIK_VIDTRANSCODE_CV_OutArgsAlg alg;
+} TRIK_VIDTRANSCODE_CV_OutArgs;
+
+/* XDM1_AlgBufInfo subset filled by GETSTATUS/GETBUFINFO (WFXNS:287-297) */
+typedef struct TRIK_XDM1_AlgBufInfo {
+  int32_t minNumInBufs;
+  int32_t minNumOutBufs;
+  int32_t minInBufSize[TRIK_XDM_MAX_IO_BUFFERS];
+  int32_t minOutBufSize[TRIK_XDM_MAX_IO_BUFFERS];
+} TRIK_XDM1_AlgBufInfo;
+
+/* IVIDTRANSCODE_Status */
+typedef struct TRIK_IVIDTRANSCODE_Status {
+  int32_t size;
+  int32_t extendedError;
+  TRIK_XDM1_SingleBufDesc data;
+  TRIK_XDM1_AlgBufInfo bufInfo;
+} TRIK_IVIDTRANSCODE_Status;
+
+typedef struct TrikCvHandle* TRIK_VIDTRANSCODE_CV_Handle;
+
+/* ---------------------------------------------------------------------- */
+/* Layer 1: XDAIS-shaped quartet                                           */
+/* ---------------------------------------------------------------------- */
+
+/* Replaces TRIK_VIDTRANSCODE_CV_alloc + _initObj (WFXNS:85-102, 146-166) as
+ * driven by Codec Engine's VIDTRANSCODE_create.  params == NULL takes the
+ * defaults of WGLUE:153-184 (YUV422 in, RGB565X out, 640x480 max; the cap is
+ * a parameter, not a static buffer size, here).  The handle binds to the
+ * calling thread's current HIP device.  Returns IALG_EOK / IALG_EFAIL. */
+int32_t TRIK_VIDTRANSCODE_CV_create(const TRIK_VIDTRANSCODE_CV_Params* params,
+                                    TRIK_VIDTRANSCODE_CV_Handle* out_handle);
+
+/* Replaces TRIK_VIDTRANSCODE_CV_free (WFXNS:114-136). */
+int32_t TRIK_VIDTRANSCODE_CV_delete(TRIK_VIDTRANSCODE_CV_Handle handle);
+
+/* Replaces TRIK_VIDTRANSCODE_CV_process (WFXNS:174-264).  One host frame in
+ * (in_bufs->descs[0]), targetX/Y/Size out in out_args->alg.  The preview
+ * stream is zero-filled (WFXNS:234) but not rendered; numOutputStreams == 0
+ * is accepted and writes nothing.  Returns IVIDTRANSCODE_EOK / _EFAIL /
+ * _EUNSUPPORTED with the reference's extendedError bits. */
+int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle handle,
+                                     TRIK_XDM1_BufDesc* in_bufs, TRIK_XDM_BufDesc* out_bufs,
+                                     TRIK_VIDTRANSCODE_CV_InArgs* in_args,
+                                     TRIK_VIDTRANSCODE_CV_OutArgs* out_args);
+
+/* Replaces TRIK_VIDTRANSCODE_CV_control (WFXNS:272-334): GETSTATUS,
+ * GETBUFINFO, SETPARAMS (re-runs setup, WGLUE:202-286), RESET/SETDEFAULT,
+ * FLUSH, GETVERSION ("1.00.00.00"). */
+int32_t TRIK_VIDTRANSCODE_CV_control(TRIK_VIDTRANSCODE_CV_Handle handle, int32_t cmd,
+                                     TRIK_VIDTRANSCODE_CV_DynamicParams* dyn_params,
+                                     TRIK_IVIDTRANSCODE_Status* status);
+
+/* ---------------------------------------------------------------------- */
+/* Layer 2: batched device API                                             */
+/* ---------------------------------------------------------------------- */
+
+#define TRIK_HSV_LAYOUT_YUYV 0   /* packed Y0 U Y1 V, row = 2*W bytes (WSEQ:251-284) */
+#define TRIK_HSV_LAYOUT_OV7670 1 /* Y plane rows + chroma plane rows; U = odd, V = even
+                                    chroma byte (OSEQ:343-387) */
+
+/* N frames in device memory: frame i starts at frames + i * frame_stride.
+ * One frame is height * line_length bytes (YUYV) or 2 * height * line_length
+ * (ov7670, chroma plane right after the luma plane).  Geometry rules of
+ * WSEQ:365-369: width % 32 == 0, height % 4 == 0, both >= 0; line_length >=
+ * 2*width (YUYV) or >= width (ov7670). */
+typedef struct TrikHsvFrameBatch {
+  const void* frames;
+  int64_t frame_stride;
+  int32_t n_frames;
+  int32_t width;
+  int32_t height;
+  int32_t line_length;
+  int32_t layout;
+} TrikHsvFrameBatch;
+
+/* Per frame per range: the reference's m_targetPoints / m_targetX / m_targetY
+ * (WSEQ:56-58, accumulated at WSEQ:350-352), widened to 64 bits. */
+typedef struct TrikHsvTargetSums {
+  int64_t points;
+  int64_t sum_x;
+  int64_t sum_y;
+} TrikHsvTargetSums;
+
+/* Per frame per range: OutArgsAlg.targetX/targetY/targetSize (WSEQ:486-505). */
+typedef struct TrikHsvTarget {
+  int8_t x;
+  int8_t y;
+  uint8_t size;
+  uint8_t reserved;
+} TrikHsvTarget;
+
+#define TRIK_HSV_MAX_RANGES 64
+
+const char* trik_hsv_version(void);
+/* Message of the last failed call on this thread ("" if none). */
+const char* trik_hsv_last_error(void);
+
+/* Full batched process: zero sums, detect + reduce, epilogue.
+ * sums_dev: [n_frames][n_ranges] TrikHsvTargetSums (device).
+ * targets_dev: [n_frames][n_ranges] TrikHsvTarget (device) or NULL.
+ * Returns 0 or TRIK_IVIDTRANSCODE_EFAIL (see trik_hsv_last_error()). */
+int32_t trik_hsv_process_batch(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvFrameBatch* batch,
+                               const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int32_t n_ranges,
+                               TrikHsvTargetSums* sums_dev, TrikHsvTarget* targets_dev,
+                               void* hip_stream);
+
+/* Detect + reduce only; ADDS into sums_dev (caller zeroes it).  This is the
+ * hot kernel, one launch per group of <= 4 ranges. */
+int32_t trik_hsv_batch_sums(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvFrameBatch* batch,
+                            const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int32_t n_ranges,
+                            TrikHsvTargetSums* sums_dev, void* hip_stream);
+
+/* Epilogue only: sums_dev -> targets_dev for an n_frames x n_ranges grid. */
+int32_t trik_hsv_batch_targets(const TrikHsvFrameBatch* batch, int32_t n_ranges,
+                               const TrikHsvTargetSums* sums_dev, TrikHsvTarget* targets_dev,
+                               void* hip_stream);
+
+/* Verification mode of the hot kernel: also writes the per-pixel detection
+ * mask (bit t = range t, n_ranges <= 8) to masks_dev[n_frames][height][width]
+ * and adds into sums_dev.  Not used on the timed path. */
+int32_t trik_hsv_batch_masks(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvFrameBatch* batch,
+                             const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int32_t n_ranges,
+                             uint8_t* masks_dev, TrikHsvTargetSums* sums_dev, void* hip_stream);
+
+/* Fill batch->frames (device, writable) with synthetic frames; frame i of the
+ * batch is global frame first_frame + i.  kind 0 = uniform random bytes,
+ * kind 1 = scene (gradients + 6 coloured discs).  Same bytes as the CPU
+ * generator in oracle/trik_oracle.c for the same (seed, frame). */
+int32_t trik_hsv_synth(const TrikHsvFrameBatch* batch, int32_t first_frame, int32_t kind,
+                       uint64_t seed, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TRIK_HSV_H_ */

@@ -1,0 +1,83 @@
+"""CPU-only checks of the C ABI: the library loads, exports every function
+include/trik_hsv.h declares, and the ctypes mirror has the C layout.  No
+compute calls (there is no GPU here)."""
+import ctypes as C
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "trik_hsv.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(\w+)\s*\(", src, flags=re.M)
+    return sorted(set(n for n in names if n not in ("if", "while")))
+
+
+@pytest.fixture(scope="module")
+def abi():
+    from trik_hsv import _abi
+
+    return _abi
+
+
+def test_header_declares_the_quartet_and_batch_api():
+    names = declared_functions()
+    for n in ("TRIK_VIDTRANSCODE_CV_create", "TRIK_VIDTRANSCODE_CV_delete",
+              "TRIK_VIDTRANSCODE_CV_process", "TRIK_VIDTRANSCODE_CV_control",
+              "trik_hsv_process_batch", "trik_hsv_batch_sums", "trik_hsv_batch_targets",
+              "trik_hsv_batch_masks", "trik_hsv_synth", "trik_hsv_version", "trik_hsv_last_error"):
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol(abi):
+    lib = abi.load()
+    for n in declared_functions():
+        assert hasattr(lib, n), n
+        assert n in abi.PROTOTYPES, f"ctypes mirror lacks {n}"
+
+
+def test_version_without_gpu(abi):
+    assert b"gfx950" in abi.load().trik_hsv_version()
+    assert abi.load().trik_hsv_last_error() == b""
+
+
+STRUCTS = ["TRIK_VIDTRANSCODE_CV_Params", "TRIK_VIDTRANSCODE_CV_DynamicParams",
+           "TRIK_VIDTRANSCODE_CV_InArgsAlg", "TRIK_VIDTRANSCODE_CV_InArgs",
+           "TRIK_VIDTRANSCODE_CV_OutArgsAlg", "TRIK_VIDTRANSCODE_CV_OutArgs",
+           "TRIK_XDM1_BufDesc", "TRIK_XDM_BufDesc", "TRIK_IVIDTRANSCODE_Status",
+           "TrikHsvFrameBatch", "TrikHsvTargetSums", "TrikHsvTarget"]
+MIRRORS = ["Params", "DynamicParams", "InArgsAlg", "InArgs", "OutArgsAlg", "OutArgs",
+           "BufDesc1", "BufDesc", "Status", "FrameBatch", "TargetSums", "Target"]
+
+
+def test_struct_layout_matches_c(abi):
+    prog = "#include <stdio.h>\n#include \"trik_hsv.h\"\nint main(void){\n"
+    for s in STRUCTS:
+        prog += f'  printf("%zu\\n", sizeof({s}));\n'
+    prog += '  printf("%zu %zu\\n", offsetof(TRIK_VIDTRANSCODE_CV_OutArgs, alg), ' \
+            'offsetof(TRIK_VIDTRANSCODE_CV_InArgs, alg));\n  return 0;\n}\n'
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "sz.c")
+        open(c, "w").write(prog.replace("#include <stdio.h>", "#include <stdio.h>\n#include <stddef.h>"))
+        exe = os.path.join(d, "sz")
+        subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split()
+    sizes = [int(x) for x in out[: len(STRUCTS)]]
+    for s, m, n in zip(STRUCTS, MIRRORS, sizes):
+        assert C.sizeof(getattr(abi, m)) == n, (s, C.sizeof(getattr(abi, m)), n)
+    assert int(out[-2]) == abi.OutArgs.alg.offset and int(out[-1]) == abi.InArgs.alg.offset
+
+
+def test_header_compiles_as_cxx():
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "h.cpp")
+        open(c, "w").write('#include "trik_hsv.h"\nint main(){return TRIK_IALG_EOK;}\n')
+        subprocess.run(["g++", "-std=c++11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                        c, "-o", os.path.join(d, "h")], check=True)

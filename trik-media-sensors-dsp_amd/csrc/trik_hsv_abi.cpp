@@ -1,0 +1,512 @@
+// trik_hsv_abi.cpp -- C ABI of libtrik_hsv.so (declared in include/trik_hsv.h).
+//
+// Layer 1 restates the reference's XDAIS codec shell and handle glue:
+//   WFXNS trik/webcam/object_sensor/src/vidtranscode_cv_fxns.c
+//   WGLUE trik/webcam/object_sensor/src/vidtranscode_cv.cpp
+// with per-handle state (the reference keeps its image buffers and LUT
+// pointers in process-wide statics, WSEQ:23-26,63-64) and the pixel work on
+// the GPU.  Layer 2 (trik_hsv_*) is the batched device API the GPU work sits
+// behind.  No C++ exception escapes any entry point.
+#include <hip/hip_runtime.h>
+#include <limits.h>
+#include <string.h>
+
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "trik_hsv_internal.h"
+
+using namespace trik_hsv;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int32_t fail(int32_t code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                  \
+  do {                                                                                 \
+    hipError_t e_ = (hipError_t)(expr);                                                \
+    if (e_ != hipSuccess)                                                              \
+      return fail(TRIK_IVIDTRANSCODE_EFAIL, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+const char k_version[] = "1.00.00.00";  // WFXNS:75
+
+const TRIK_VIDTRANSCODE_CV_Params k_default_params = {{
+    (int32_t)sizeof(TRIK_VIDTRANSCODE_CV_Params),  // WGLUE:153-184
+    1,
+    TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_YUV422,
+    {TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_RGB565X, TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_UNKNOWN},
+    480, 640, 60000, -1,
+    {480, -1},
+    {640, -1},
+    {-1, -1},
+    {-1, -1},
+    1 /* XDM_BYTE */}};
+
+TRIK_VIDTRANSCODE_CV_DynamicParams default_dynamic_params() {  // WGLUE:205-266
+  TRIK_VIDTRANSCODE_CV_DynamicParams d;
+  memset(&d, 0, sizeof d);
+  d.base.size = (int32_t)sizeof(TRIK_VIDTRANSCODE_CV_DynamicParams);
+  d.base.readHeaderOnlyFlag = 0;
+  d.base.keepInputResolutionFlag[0] = 0;
+  d.base.keepInputResolutionFlag[1] = 1;
+  d.base.outputHeight[0] = 240;
+  d.base.outputWidth[0] = 320;
+  d.base.keepInputFrameRateFlag[0] = d.base.keepInputFrameRateFlag[1] = 1;
+  d.base.inputFrameRate = -1;
+  d.base.outputFrameRate[0] = d.base.outputFrameRate[1] = -1;
+  d.base.targetBitRate[0] = d.base.targetBitRate[1] = -1;
+  d.base.keepInputGOPFlag[0] = d.base.keepInputGOPFlag[1] = 1;
+  d.base.intraFrameInterval[0] = d.base.intraFrameInterval[1] = 1;
+  d.base.forceFrame[0] = d.base.forceFrame[1] = -1;  // IVIDEO_NA_FRAME
+  d.inputHeight = -1;
+  d.inputWidth = -1;
+  d.inputLineLength = -1;
+  d.outputLineLength[0] = d.outputLineLength[1] = -1;
+  return d;
+}
+
+std::string validate_batch(const TrikHsvFrameBatch* b) {
+  if (!b) return "batch is NULL";
+  if (b->n_frames < 0) return "n_frames < 0";
+  if (b->width < 0 || b->height < 0 || b->width % 32 != 0 || b->height % 4 != 0)
+    return "geometry: need width % 32 == 0, height % 4 == 0, both >= 0 (WSEQ:365-369)";
+  if (b->width > 32767 || b->height > 32767) return "geometry: width/height exceed int16 (WINT:32)";
+  if (b->layout != TRIK_HSV_LAYOUT_YUYV && b->layout != TRIK_HSV_LAYOUT_OV7670) return "unknown layout";
+  const int64_t row = b->layout == TRIK_HSV_LAYOUT_YUYV ? 2LL * b->width : (int64_t)b->width;
+  if (b->height > 0 && b->line_length < row) return "line_length shorter than a row";
+  const int64_t fb = (int64_t)b->height * b->line_length * (b->layout == TRIK_HSV_LAYOUT_OV7670 ? 2 : 1);
+  if (b->n_frames > 1 && b->frame_stride < fb) return "frame_stride shorter than a frame";
+  if (b->n_frames > 0 && fb > 0 && !b->frames) return "frames is NULL";
+  return "";
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Handle
+// ---------------------------------------------------------------------------
+struct TrikCvHandle {
+  int device = 0;
+  TRIK_VIDTRANSCODE_CV_Params params{};
+  TRIK_VIDTRANSCODE_CV_DynamicParams dyn{};
+  bool alg_ready = false;  // the reference's m_cvAlgorithm is set (WGLUE:302)
+  int layout = TRIK_HSV_LAYOUT_YUYV;
+  int in_w = 0, in_h = 0, in_ll = 0;
+  int out_w = 0, out_h = 0, out_ll = 0;
+  std::mutex mu;
+
+  // compiled range tables (device) and the key they were compiled from
+  RangeTables* d_tables = nullptr;
+  int table_groups_cap = 0;
+  std::vector<uint32_t> table_key;
+  RangeTables* h_tables = nullptr;  // pinned staging
+  hipEvent_t tables_busy = nullptr;
+
+  // process() staging
+  hipStream_t stream = nullptr;
+  uint8_t* d_frame = nullptr;
+  size_t d_frame_cap = 0;
+  TrikHsvTargetSums* d_sums = nullptr;
+  TrikHsvTarget* d_targets = nullptr;
+};
+
+namespace {
+
+void release(TrikCvHandle* h) {
+  if (!h) return;
+  int prev = 0;
+  bool switched = hipGetDevice(&prev) == hipSuccess && prev != h->device &&
+                  hipSetDevice(h->device) == hipSuccess;
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->tables_busy) (void)hipEventSynchronize(h->tables_busy);
+  (void)hipFree(h->d_tables);
+  (void)hipHostFree(h->h_tables);
+  (void)hipFree(h->d_frame);
+  (void)hipFree(h->d_sums);
+  (void)hipFree(h->d_targets);
+  if (h->tables_busy) (void)hipEventDestroy(h->tables_busy);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  if (switched) (void)hipSetDevice(prev);
+  delete h;
+}
+
+// handleSetupImageDesc + createCVAlgorithm + BallDetector::setup
+// (WGLUE:52-145, WSEQ:358-410).
+int32_t setup_image_desc(TrikCvHandle* h) {
+  h->alg_ready = false;
+  const TRIK_IVIDTRANSCODE_Params& p = h->params.base;
+  if (p.numOutputStreams != 0 && p.numOutputStreams != 1)  // WGLUE:96-101
+    return fail(TRIK_IALG_EFAIL, "invalid number of output streams");
+  const int in_fmt = p.formatInput;
+  const int in_w = h->dyn.inputWidth > 0 ? h->dyn.inputWidth : 0;  // WGLUE:106-109
+  const int in_h = h->dyn.inputHeight > 0 ? h->dyn.inputHeight : 0;
+  const int in_ll = h->dyn.inputLineLength > 0 ? h->dyn.inputLineLength : 0;
+  int out_fmt = TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_UNKNOWN, out_w = 0, out_h = 0, out_ll = 0;
+  if (p.numOutputStreams == 1) {  // WGLUE:111-117
+    out_fmt = p.formatOutput[0];
+    out_w = h->dyn.base.outputWidth[0] > 0 ? h->dyn.base.outputWidth[0] : 0;
+    out_h = h->dyn.base.outputHeight[0] > 0 ? h->dyn.base.outputHeight[0] : 0;
+    out_ll = h->dyn.outputLineLength[0] > 0 ? h->dyn.outputLineLength[0] : 0;
+  }
+  if (in_w > p.maxWidthInput || in_h > p.maxHeightInput ||  // WGLUE:126-135
+      (p.numOutputStreams == 1 && (out_w > p.maxWidthOutput[0] || out_h > p.maxHeightOutput[0])))
+    return fail(TRIK_IALG_EFAIL, "invalid image dimensions");
+  // IF_IN_OUT_FORMAT dispatch (WGLUE:76-84): BallDetector<YUV422, RGB565X>
+  // (webcam) and BallDetector<YUV422P, RGB565X> (ov7670 object sensor).  With
+  // no output stream the preview format is UNKNOWN; the reference then finds
+  // no algorithm, this build accepts it (no preview to write).
+  const bool out_ok = out_fmt == TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_RGB565X ||
+                      (p.numOutputStreams == 0 && out_fmt == TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_UNKNOWN);
+  int layout;
+  if (in_fmt == TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_YUV422 && out_ok)
+    layout = TRIK_HSV_LAYOUT_YUYV;
+  else if (in_fmt == TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_YUV422P && out_ok)
+    layout = TRIK_HSV_LAYOUT_OV7670;
+  else
+    return fail(TRIK_IALG_EFAIL, "cannot create CV algorithm for this format pair");
+  if (in_w % 32 != 0 || in_h % 4 != 0 || in_w > 32767 || in_h > 32767)  // WSEQ:365-369
+    return fail(TRIK_IALG_EFAIL, "CV algorithm setup failed: width % 32 / height % 4");
+  const int row = layout == TRIK_HSV_LAYOUT_YUYV ? 2 * in_w : in_w;
+  if (in_h > 0 && in_ll < row)
+    return fail(TRIK_IALG_EFAIL, "CV algorithm setup failed: inputLineLength shorter than a row");
+  h->layout = layout;
+  h->in_w = in_w; h->in_h = in_h; h->in_ll = in_ll;
+  h->out_w = out_w; h->out_h = out_h; h->out_ll = out_ll;
+  h->alg_ready = true;
+  return TRIK_IALG_EOK;
+}
+
+int32_t setup_dynamic(TrikCvHandle* h, const TRIK_VIDTRANSCODE_CV_DynamicParams* d) {
+  h->dyn = d ? *d : default_dynamic_params();  // WGLUE:271-274
+  return setup_image_desc(h);
+}
+
+// Compile + upload the tables for ranges[0..n), stream-ordered on s.
+int32_t ensure_tables(TrikCvHandle* h, const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n,
+                      hipStream_t s) {
+  std::vector<uint32_t> key;
+  key.reserve(3 * n + 1);
+  key.push_back((uint32_t)n);
+  for (int i = 0; i < n; ++i) {
+    const PackedRange p = pack_range(ranges[i]);
+    key.push_back(p.from); key.push_back(p.to); key.push_back(p.expect);
+  }
+  if (key == h->table_key && h->d_tables) return 0;
+  const int groups = (n + kRangesPerLaunch - 1) / kRangesPerLaunch;
+  if (h->tables_busy) HIP_TRY(hipEventSynchronize(h->tables_busy));  // previous users done
+  if (groups > h->table_groups_cap) {
+    (void)hipFree(h->d_tables);
+    (void)hipHostFree(h->h_tables);
+    h->d_tables = nullptr; h->h_tables = nullptr; h->table_groups_cap = 0;
+    HIP_TRY(hipMalloc(&h->d_tables, sizeof(RangeTables) * groups));
+    HIP_TRY(hipHostMalloc(&h->h_tables, sizeof(RangeTables) * groups, hipHostMallocDefault));
+    h->table_groups_cap = groups;
+  }
+  for (int g = 0; g < groups; ++g) {
+    const int cnt = n - g * kRangesPerLaunch < kRangesPerLaunch ? n - g * kRangesPerLaunch : kRangesPerLaunch;
+    compile_tables(ranges + g * kRangesPerLaunch, cnt, &h->h_tables[g]);
+  }
+  HIP_TRY(hipMemcpyAsync(h->d_tables, h->h_tables, sizeof(RangeTables) * groups,
+                         hipMemcpyHostToDevice, s));
+  h->table_key.swap(key);
+  return 0;
+}
+
+int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
+                 const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, TrikHsvTargetSums* sums,
+                 uint8_t* masks, hipStream_t s) {
+  int32_t rc = ensure_tables(h, ranges, n, s);
+  if (rc) return rc;
+  if (b->n_frames == 0 || b->width == 0 || b->height == 0) return 0;
+  for (int g = 0; g * kRangesPerLaunch < n; ++g) {
+    KernelArgs a;
+    a.frames = static_cast<const uint8_t*>(b->frames);
+    a.frame_stride = b->n_frames > 1 ? b->frame_stride : 0;
+    a.n_frames = b->n_frames;
+    a.width = b->width; a.height = b->height; a.line_length = b->line_length;
+    a.layout = b->layout;
+    a.n_ranges = n - g * kRangesPerLaunch < kRangesPerLaunch ? n - g * kRangesPerLaunch : kRangesPerLaunch;
+    a.range_offset = g * kRangesPerLaunch;
+    a.sums_ranges = n;
+    a.tables = h->d_tables + g;
+    a.sums = sums;
+    a.masks = masks;
+    a.mask_shift = g * kRangesPerLaunch;
+    HIP_TRY(launch_reduce(a, masks != nullptr, s));
+  }
+  if (!h->tables_busy) HIP_TRY(hipEventCreateWithFlags(&h->tables_busy, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(h->tables_busy, s));
+  return 0;
+}
+
+inline void set_bit(int32_t& word, int bit) { word |= (int32_t)(1u << bit); }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Layer 1: XDAIS-shaped quartet
+// ---------------------------------------------------------------------------
+extern "C" int32_t TRIK_VIDTRANSCODE_CV_create(const TRIK_VIDTRANSCODE_CV_Params* params,
+                                               TRIK_VIDTRANSCODE_CV_Handle* out_handle) {
+  if (!out_handle) return fail(TRIK_IALG_EFAIL, "out_handle is NULL");
+  *out_handle = nullptr;
+  TrikCvHandle* h = new (std::nothrow) TrikCvHandle();
+  if (!h) return fail(TRIK_IALG_EFAIL, "out of memory");
+  if (hipGetDevice(&h->device) != hipSuccess) {
+    delete h;
+    return fail(TRIK_IALG_EFAIL, "no HIP device");
+  }
+  h->params = params ? *params : k_default_params;  // WGLUE:188-191
+  const int32_t rc = setup_dynamic(h, nullptr);      // WFXNS:158-163
+  if (rc != TRIK_IALG_EOK) {
+    release(h);
+    return rc;
+  }
+  *out_handle = h;
+  return TRIK_IALG_EOK;
+}
+
+extern "C" int32_t TRIK_VIDTRANSCODE_CV_delete(TRIK_VIDTRANSCODE_CV_Handle handle) {
+  if (!handle) return fail(TRIK_IALG_EFAIL, "handle is NULL");
+  release(handle);
+  return TRIK_IALG_EOK;
+}
+
+extern "C" int32_t TRIK_VIDTRANSCODE_CV_control(TRIK_VIDTRANSCODE_CV_Handle h, int32_t cmd,
+                                                TRIK_VIDTRANSCODE_CV_DynamicParams* dyn,
+                                                TRIK_IVIDTRANSCODE_Status* status) {
+  if (!h || !status) return fail(TRIK_IVIDTRANSCODE_EFAIL, "handle or status is NULL");
+  std::lock_guard<std::mutex> lock(h->mu);
+  int32_t rc = TRIK_IVIDTRANSCODE_EFAIL;
+  status->data.accessMask &= ~((1 << TRIK_XDM_ACCESSMODE_READ) | (1 << TRIK_XDM_ACCESSMODE_WRITE));
+  switch (cmd) {  // WFXNS:285-331
+    case TRIK_XDM_GETSTATUS:
+    case TRIK_XDM_GETBUFINFO:
+      status->extendedError = 0;
+      status->bufInfo.minNumInBufs = 1;
+      status->bufInfo.minNumOutBufs = 1;
+      status->bufInfo.minInBufSize[0] = 0;
+      status->bufInfo.minOutBufSize[0] = 0;
+      set_bit(status->data.accessMask, TRIK_XDM_ACCESSMODE_WRITE);
+      rc = TRIK_IVIDTRANSCODE_EOK;
+      break;
+    case TRIK_XDM_SETPARAMS:
+      if (dyn && dyn->base.size == (int32_t)sizeof(TRIK_VIDTRANSCODE_CV_DynamicParams))
+        rc = setup_dynamic(h, dyn);
+      else
+        rc = fail(TRIK_IVIDTRANSCODE_EUNSUPPORTED, "SETPARAMS: dynamic params size mismatch");
+      break;
+    case TRIK_XDM_RESET:
+    case TRIK_XDM_SETDEFAULT:
+      rc = setup_dynamic(h, nullptr);
+      break;
+    case TRIK_XDM_FLUSH:
+      rc = TRIK_IVIDTRANSCODE_EOK;
+      break;
+    case TRIK_XDM_GETVERSION:
+      if (status->data.buf && status->data.bufSize >= (int32_t)sizeof k_version) {
+        memcpy(status->data.buf, k_version, sizeof k_version);
+        set_bit(status->data.accessMask, TRIK_XDM_ACCESSMODE_WRITE);
+        rc = TRIK_IVIDTRANSCODE_EOK;
+      } else {
+        rc = fail(TRIK_IVIDTRANSCODE_EFAIL, "GETVERSION: buffer too small");
+      }
+      break;
+    default:
+      rc = fail(TRIK_IVIDTRANSCODE_EFAIL, "unsupported control command");
+  }
+  return rc;
+}
+
+extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
+                                                TRIK_XDM1_BufDesc* in_bufs,
+                                                TRIK_XDM_BufDesc* out_bufs,
+                                                TRIK_VIDTRANSCODE_CV_InArgs* in_args,
+                                                TRIK_VIDTRANSCODE_CV_OutArgs* out_args) {
+  if (!h || !in_bufs || !out_bufs || !in_args || !out_args)
+    return fail(TRIK_IVIDTRANSCODE_EFAIL, "NULL argument");
+  std::lock_guard<std::mutex> lock(h->mu);
+  if (in_args->base.size != (int32_t)sizeof(TRIK_VIDTRANSCODE_CV_InArgs) ||  // WFXNS:192-197
+      out_args->base.size != (int32_t)sizeof(TRIK_VIDTRANSCODE_CV_OutArgs)) {
+    set_bit(out_args->base.extendedError, TRIK_XDM_UNSUPPORTEDPARAM_BIT);
+    return fail(TRIK_IVIDTRANSCODE_EUNSUPPORTED, "InArgs/OutArgs size mismatch");
+  }
+  if (in_bufs->numBufs != 1 || out_bufs->numBufs < h->params.base.numOutputStreams) {  // :199-204
+    set_bit(out_args->base.extendedError, TRIK_XDM_UNSUPPORTEDPARAM_BIT);
+    return fail(TRIK_IVIDTRANSCODE_EFAIL, "buffer count");
+  }
+  TRIK_XDM1_SingleBufDesc* in = &in_bufs->descs[0];
+  if (!in->buf || in_args->base.numBytes < 0 || in_args->base.numBytes > in->bufSize) {  // :207-214
+    set_bit(out_args->base.extendedError, TRIK_XDM_UNSUPPORTEDPARAM_BIT);
+    return fail(TRIK_IVIDTRANSCODE_EFAIL, "input buffer");
+  }
+  set_bit(in->accessMask, TRIK_XDM_ACCESSMODE_READ);  // :216-221
+  out_args->base.bitsConsumed = in_args->base.numBytes * CHAR_BIT;
+  out_args->base.decodedPictureType = -1;       // IVIDEO_NA_PICTURE
+  out_args->base.decodedPictureStructure = -1;  // IVIDEO_CONTENTTYPE_NA
+  out_args->base.decodedHeight = h->dyn.inputHeight;
+  out_args->base.decodedWidth = h->dyn.inputWidth;
+  const int64_t in_size = in_args->base.numBytes;
+
+  TRIK_XDM1_SingleBufDesc* out = nullptr;
+  int8_t* out_ptr = nullptr;
+  int64_t out_size = 0;
+  if (h->params.base.numOutputStreams == 1) {  // :226-235
+    out = &out_args->base.encodedBuf[0];
+    out->buf = out_bufs->bufs ? out_bufs->bufs[0] : nullptr;
+    out->bufSize = out_bufs->bufSizes ? out_bufs->bufSizes[0] : 0;
+    out->accessMask = 0;
+    out_ptr = out->buf;
+    out_size = out->bufSize;
+    if (out_ptr && out_size > 0) memset(out_ptr, 0, (size_t)out_size);
+  }
+
+  // trikCvProceedImage + BallDetector::run (WGLUE:291-320, WSEQ:412-508)
+  int32_t rc = TRIK_IVIDTRANSCODE_EOK;
+  std::string why;
+  if (!h->alg_ready) {
+    rc = TRIK_IVIDTRANSCODE_EFAIL; why = "CV algorithm not created";
+  } else if ((int64_t)h->in_h * h->in_ll > in_size ||
+             (h->layout == TRIK_HSV_LAYOUT_OV7670 && 2LL * h->in_h * h->in_ll > in_size)) {
+    rc = TRIK_IVIDTRANSCODE_EFAIL; why = "input buffer smaller than the image";  // WSEQ:415-416
+  } else if ((int64_t)h->out_h * h->out_ll > out_size) {
+    rc = TRIK_IVIDTRANSCODE_EFAIL; why = "output buffer smaller than the preview";  // WSEQ:417-418
+  }
+  if (rc == TRIK_IVIDTRANSCODE_EOK) {
+    out_size = (int64_t)h->out_h * h->out_ll;  // WSEQ:419
+    TRIK_VIDTRANSCODE_CV_OutArgsAlg& oa = out_args->alg;
+    oa.targetX = 0; oa.targetY = 0; oa.targetSize = 0;
+    if (h->in_w > 0 && h->in_h > 0) {
+      int prev = 0;
+      const bool switched = hipGetDevice(&prev) == hipSuccess && prev != h->device;
+      if (switched) (void)hipSetDevice(h->device);
+      const size_t fb = (size_t)h->in_h * h->in_ll * (h->layout == TRIK_HSV_LAYOUT_OV7670 ? 2 : 1);
+      auto body = [&]() -> int32_t {
+        if (!h->stream) HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+        if (fb > h->d_frame_cap) {
+          (void)hipFree(h->d_frame);
+          h->d_frame = nullptr; h->d_frame_cap = 0;
+          HIP_TRY(hipMalloc(&h->d_frame, fb));
+          h->d_frame_cap = fb;
+        }
+        if (!h->d_sums) HIP_TRY(hipMalloc(&h->d_sums, sizeof(TrikHsvTargetSums)));
+        if (!h->d_targets) HIP_TRY(hipMalloc(&h->d_targets, sizeof(TrikHsvTarget)));
+        HIP_TRY(hipMemcpyAsync(h->d_frame, in->buf, fb, hipMemcpyHostToDevice, h->stream));
+        TrikHsvFrameBatch b = {h->d_frame, (int64_t)fb, 1, h->in_w, h->in_h, h->in_ll, h->layout};
+        HIP_TRY(hipMemsetAsync(h->d_sums, 0, sizeof(TrikHsvTargetSums), h->stream));
+        int32_t r = run_sums(h, &b, &in_args->alg, 1, h->d_sums, nullptr, h->stream);
+        if (r) return r;
+        HIP_TRY(launch_targets(b, 1, h->d_sums, h->d_targets, h->stream));
+        TrikHsvTarget t;
+        HIP_TRY(hipMemcpyAsync(&t, h->d_targets, sizeof t, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        oa.targetX = t.x; oa.targetY = t.y; oa.targetSize = t.size;
+        return 0;
+      };
+      const int32_t r = body();
+      if (switched) (void)hipSetDevice(prev);
+      if (r) { rc = TRIK_IVIDTRANSCODE_EFAIL; why = g_last_error; }
+    }
+    // autoDetectHsv (WSEQ:455-462) is not implemented: OutArgs.detect* are
+    // left untouched, as the reference does when the flag is clear.
+  }
+  if (rc != TRIK_IVIDTRANSCODE_EOK) {
+    set_bit(out_args->base.extendedError, TRIK_XDM_CORRUPTEDDATA_BIT);  // WFXNS:243-247
+    return fail(rc, why);
+  }
+  if (out) {  // WFXNS:249-259
+    out->bufSize = (int32_t)out_size;
+    set_bit(out->accessMask, TRIK_XDM_ACCESSMODE_WRITE);
+    out_args->base.bitsGenerated[0] = out->bufSize * CHAR_BIT;
+    out_args->base.encodedPictureType[0] = out_args->base.decodedPictureType;
+    out_args->base.encodedPictureStructure[0] = out_args->base.decodedPictureStructure;
+    out_args->base.outputID[0] = in_args->base.inputID;
+    out_args->base.inputFrameSkipTranscodeFlag[0] = 0;
+  }
+  out_args->base.outBufsInUseFlag = 0;
+  return TRIK_IVIDTRANSCODE_EOK;
+}
+
+// ---------------------------------------------------------------------------
+// Layer 2: batched device API
+// ---------------------------------------------------------------------------
+extern "C" const char* trik_hsv_version(void) { return "trik-hsv-mi355x 0.1.0 (gfx950)"; }
+
+extern "C" const char* trik_hsv_last_error(void) { return g_last_error.c_str(); }
+
+static int32_t check_common(TRIK_VIDTRANSCODE_CV_Handle h, const TrikHsvFrameBatch* b,
+                            const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int32_t n,
+                            const void* sums) {
+  if (!h) return fail(TRIK_IVIDTRANSCODE_EFAIL, "handle is NULL");
+  const std::string e = validate_batch(b);
+  if (!e.empty()) return fail(TRIK_IVIDTRANSCODE_EFAIL, e);
+  if (n < 1 || n > TRIK_HSV_MAX_RANGES || !ranges)
+    return fail(TRIK_IVIDTRANSCODE_EFAIL, "n_ranges must be 1..64");
+  if (!sums && b->n_frames > 0) return fail(TRIK_IVIDTRANSCODE_EFAIL, "sums is NULL");
+  return 0;
+}
+
+extern "C" int32_t trik_hsv_batch_sums(TRIK_VIDTRANSCODE_CV_Handle h, const TrikHsvFrameBatch* b,
+                                       const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int32_t n,
+                                       TrikHsvTargetSums* sums, void* stream) {
+  int32_t rc = check_common(h, b, ranges, n, sums);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lock(h->mu);
+  return run_sums(h, b, ranges, n, sums, nullptr, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int32_t trik_hsv_batch_targets(const TrikHsvFrameBatch* b, int32_t n,
+                                          const TrikHsvTargetSums* sums, TrikHsvTarget* targets,
+                                          void* stream) {
+  const std::string e = validate_batch(b);
+  if (!e.empty()) return fail(TRIK_IVIDTRANSCODE_EFAIL, e);
+  if (n < 1 || n > TRIK_HSV_MAX_RANGES) return fail(TRIK_IVIDTRANSCODE_EFAIL, "n_ranges must be 1..64");
+  if (b->n_frames > 0 && (!sums || !targets)) return fail(TRIK_IVIDTRANSCODE_EFAIL, "NULL buffer");
+  HIP_TRY(launch_targets(*b, n, sums, targets, static_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+extern "C" int32_t trik_hsv_process_batch(TRIK_VIDTRANSCODE_CV_Handle h, const TrikHsvFrameBatch* b,
+                                          const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int32_t n,
+                                          TrikHsvTargetSums* sums, TrikHsvTarget* targets,
+                                          void* stream) {
+  int32_t rc = check_common(h, b, ranges, n, sums);
+  if (rc) return rc;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  std::lock_guard<std::mutex> lock(h->mu);
+  if (b->n_frames > 0)
+    HIP_TRY(hipMemsetAsync(sums, 0, sizeof(TrikHsvTargetSums) * (size_t)b->n_frames * n, s));
+  rc = run_sums(h, b, ranges, n, sums, nullptr, s);
+  if (rc) return rc;
+  if (targets) HIP_TRY(launch_targets(*b, n, sums, targets, s));
+  return 0;
+}
+
+extern "C" int32_t trik_hsv_batch_masks(TRIK_VIDTRANSCODE_CV_Handle h, const TrikHsvFrameBatch* b,
+                                        const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int32_t n,
+                                        uint8_t* masks, TrikHsvTargetSums* sums, void* stream) {
+  int32_t rc = check_common(h, b, ranges, n, sums);
+  if (rc) return rc;
+  if (n > 8) return fail(TRIK_IVIDTRANSCODE_EFAIL, "mask mode supports at most 8 ranges");
+  if (!masks && b->n_frames > 0) return fail(TRIK_IVIDTRANSCODE_EFAIL, "masks is NULL");
+  std::lock_guard<std::mutex> lock(h->mu);
+  return run_sums(h, b, ranges, n, sums, masks, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int32_t trik_hsv_synth(const TrikHsvFrameBatch* b, int32_t first_frame, int32_t kind,
+                                  uint64_t seed, void* stream) {
+  const std::string e = validate_batch(b);
+  if (!e.empty()) return fail(TRIK_IVIDTRANSCODE_EFAIL, e);
+  if (kind != 0 && kind != 1) return fail(TRIK_IVIDTRANSCODE_EFAIL, "kind must be 0 or 1");
+  HIP_TRY(launch_synth(*b, const_cast<uint8_t*>(static_cast<const uint8_t*>(b->frames)), first_frame,
+                       kind, seed, static_cast<hipStream_t>(stream)));
+  return 0;
+}

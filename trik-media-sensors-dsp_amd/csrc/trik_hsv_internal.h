@@ -1,0 +1,60 @@
+// trik_hsv_internal.h -- shared between the host C++ (ABI, table compiler)
+// and the HIP kernels.  Not part of the public ABI (include/trik_hsv.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/trik_hsv.h"
+
+namespace trik_hsv {
+
+// Ranges handled by one launch of the hot kernel (per-pixel masks are
+// byte-spread: range t -> bits 8t..8t+7 of a 32-bit word).
+constexpr int kRangesPerLaunch = 4;
+
+// Device-side lookup tables compiled from one group of <= 4 ranges
+// (trik_hsv_tables.cpp).  Staged into LDS by every workgroup.
+//   sv[mx * 256 + mn] : bit t = range t's saturation AND value tests pass for a
+//                       pixel with max channel mx and min channel mn (mn <= mx).
+//                       S = (LUT255[mx] * (mx - mn)) >> 8 (WSEQ:223-224), V = mx.
+//   hue[H]            : bit t = range t's hue test passes (incl. wrap, WSEQ:433-445).
+//   lut43[d]          : s_mult43_div (WSEQ:389-407).
+struct alignas(16) RangeTables {
+  uint8_t sv[256 * 256];
+  uint8_t hue[256];
+  uint16_t lut43[256];
+};
+static_assert(sizeof(RangeTables) == 65536 + 256 + 512, "table layout");
+
+// Packed form of one InArgs range (WSEQ:425-445).
+struct PackedRange {
+  uint32_t from, to, expect;
+};
+
+PackedRange pack_range(const TRIK_VIDTRANSCODE_CV_InArgsAlg& r);
+void compile_tables(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTables* out);
+
+struct KernelArgs {
+  const uint8_t* frames;
+  int64_t frame_stride;
+  int32_t n_frames;
+  int32_t width, height, line_length;
+  int32_t layout;
+  int32_t n_ranges;      // ranges in this launch (1..4)
+  int32_t range_offset;  // index of this launch's first range in the sums array
+  int32_t sums_ranges;   // ranges per frame in the sums array (row pitch)
+  const RangeTables* tables;
+  TrikHsvTargetSums* sums;
+  uint8_t* masks;        // verification mode only
+  int32_t mask_shift;    // bit position of this launch's range 0 in the mask byte
+};
+
+// Launchers (trik_hsv_kernels.hip).  Return hipError_t as int.
+int launch_reduce(const KernelArgs& a, bool write_masks, hipStream_t s);
+int launch_targets(const TrikHsvFrameBatch& b, int n_ranges, const TrikHsvTargetSums* sums,
+                   TrikHsvTarget* targets, hipStream_t s);
+int launch_synth(const TrikHsvFrameBatch& b, uint8_t* frames, int first_frame, int kind,
+                 uint64_t seed, hipStream_t s);
+
+}  // namespace trik_hsv

@@ -1,0 +1,70 @@
+// trik_hsv_tables.cpp -- host-side "range compiler": turns a group of InArgs
+// HSV ranges into the LDS lookup tables the hot kernel uses.
+//
+// The reference tests a packed HSV word against packed bounds per pixel
+// (detectHsvPixel, WSEQ:171-179): mask = cmpltu4(hsv, from) | cmpgtu4(hsv, to),
+// det = (mask == expect).  The H, S and V lanes of that mask are independent,
+// so det = hue_ok(H) && sat_ok(S) && val_ok(V) with
+//   hue_ok(H) = ((H < from.H) || (H > to.H)) == expect.bit0
+//   sat_ok(S) = !((S < from.S) || (S > to.S)),   val_ok likewise,
+// which is exactly what the tables below enumerate.
+#include <string.h>
+
+#include "trik_hsv_internal.h"
+
+namespace trik_hsv {
+
+static inline int32_t clamp_range(int32_t lo, int32_t v, int32_t hi) {  // stdcpp.hpp:38-44
+  return v < lo ? lo : (v > hi ? hi : v);
+}
+
+PackedRange pack_range(const TRIK_VIDTRANSCODE_CV_InArgsAlg& r) {  // WSEQ:425-445
+  const uint32_t hf = (uint32_t)clamp_range(0, ((int32_t)r.detectHueFrom * 255) / 359, 255);
+  const uint32_t ht = (uint32_t)clamp_range(0, ((int32_t)r.detectHueTo * 255) / 359, 255);
+  const uint32_t sf = (uint32_t)clamp_range(0, ((int32_t)r.detectSatFrom * 255) / 100, 255);
+  const uint32_t st = (uint32_t)clamp_range(0, ((int32_t)r.detectSatTo * 255) / 100, 255);
+  const uint32_t vf = (uint32_t)clamp_range(0, ((int32_t)r.detectValFrom * 255) / 100, 255);
+  const uint32_t vt = (uint32_t)clamp_range(0, ((int32_t)r.detectValTo * 255) / 100, 255);
+  PackedRange p;
+  if (hf <= ht) {
+    p.from = (vf << 16) | (sf << 8) | hf;
+    p.to = (vt << 16) | (st << 8) | ht;
+    p.expect = 0;
+  } else {  // hue wrap through 0
+    p.from = (vf << 16) | (sf << 8) | ((ht + 1) & 0xFF);
+    p.to = (vt << 16) | (st << 8) | ((hf - 1) & 0xFF);
+    p.expect = 1;
+  }
+  return p;
+}
+
+static inline bool outside(uint32_t x, uint32_t lo, uint32_t hi) { return x < lo || x > hi; }
+
+void compile_tables(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTables* out) {
+  memset(out, 0, sizeof(*out));
+  out->lut43[0] = 0;
+  uint16_t lut255[256];
+  lut255[0] = 0;
+  for (uint32_t i = 1; i < 256; ++i) {  // WSEQ:400-406
+    out->lut43[i] = (uint16_t)((43u * 256u) / i);
+    lut255[i] = (uint16_t)((255u * 256u) / i);
+  }
+  for (int t = 0; t < n; ++t) {
+    const PackedRange p = pack_range(ranges[t]);
+    const uint8_t bit = (uint8_t)(1u << t);
+    const uint32_t fh = p.from & 0xFF, th = p.to & 0xFF;
+    const uint32_t fs = (p.from >> 8) & 0xFF, ts = (p.to >> 8) & 0xFF;
+    const uint32_t fv = (p.from >> 16) & 0xFF, tv = (p.to >> 16) & 0xFF;
+    for (uint32_t h = 0; h < 256; ++h)
+      if ((outside(h, fh, th) ? 1u : 0u) == (p.expect & 1u)) out->hue[h] |= bit;
+    for (uint32_t mx = 0; mx < 256; ++mx) {
+      if (outside(mx, fv, tv)) continue;
+      for (uint32_t mn = 0; mn <= mx; ++mn) {
+        const uint32_t s = (lut255[mx] * (mx - mn)) >> 8;
+        if (!outside(s, fs, ts)) out->sv[mx * 256 + mn] |= bit;
+      }
+    }
+  }
+}
+
+}  // namespace trik_hsv

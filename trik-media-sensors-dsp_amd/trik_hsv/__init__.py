@@ -1,0 +1,266 @@
+"""trik_hsv -- host-side mirror of the TRIK object-sensor operator, MI355X-native.
+
+Everything computes in libtrik_hsv.so (HIP kernels for gfx950 + the C++
+XDAIS-shaped layer) through its C ABI (include/trik_hsv.h).  PyTorch is used
+only to own device memory and streams.  There is no CPU fallback.
+
+Two surfaces, mirroring the reference (paths relative to the reference checkout):
+  * ObjectSensor -- the codec instance: create / control / process / delete of
+    trik/webcam/object_sensor/src/vidtranscode_cv_fxns.c, one host frame per
+    process() call, OutArgs.targetX/targetY/targetSize out.
+  * Detector -- the batched device path: N frames resident in HBM, T HSV
+    ranges, per-frame per-range {points, sumX, sumY} and targets.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Iterable, Sequence, Tuple
+
+from . import _abi
+from ._abi import (FORMAT_RGB565X, FORMAT_UNKNOWN, FORMAT_YUV422, FORMAT_YUV422P,  # noqa: F401
+                   IALG_EFAIL, IALG_EOK, IVIDTRANSCODE_EFAIL, IVIDTRANSCODE_EOK,
+                   IVIDTRANSCODE_EUNSUPPORTED, LAYOUT_OV7670, LAYOUT_YUYV, XDM_FLUSH,
+                   XDM_GETBUFINFO, XDM_GETSTATUS, XDM_GETVERSION, XDM_RESET, XDM_SETDEFAULT,
+                   XDM_SETPARAMS)
+
+_lib = _abi.load()  # fails loudly when the native library is missing
+
+Range = Tuple[int, int, int, int, int, int]  # hue_from, hue_to, sat_from, sat_to, val_from, val_to
+
+
+class TrikHsvError(RuntimeError):
+    def __init__(self, rc: int, what: str):
+        super().__init__(f"{what} failed (rc={rc}): {_abi.last_error()}")
+        self.rc = rc
+
+
+def version() -> str:
+    return _lib.trik_hsv_version().decode()
+
+
+def _ranges(ranges: Iterable[Sequence[int]]):
+    rs = [tuple(int(v) for v in r) for r in ranges]
+    arr = (_abi.InArgsAlg * max(1, len(rs)))()
+    for i, r in enumerate(rs):
+        arr[i] = _abi.InArgsAlg(*r[:6], 0)
+    return arr, len(rs)
+
+
+def frame_bytes(width: int, height: int, line_length: int, layout: int) -> int:
+    return height * line_length * (2 if layout == LAYOUT_OV7670 else 1)
+
+
+def _stream_ptr(stream) -> C.c_void_p:
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)
+
+
+def _batch(frames, width, height, line_length, layout, n_frames=None, frame_stride=None):
+    fb = frame_bytes(width, height, line_length, layout)
+    if frame_stride is None:
+        frame_stride = fb
+    if n_frames is None:
+        n_frames = frames.numel() // frame_stride if frame_stride else 0
+    if frames.dtype.itemsize != 1 or not frames.is_cuda:
+        raise ValueError("frames must be a uint8 CUDA (HIP) tensor")
+    if n_frames > 0 and (n_frames - 1) * frame_stride + fb > frames.numel():
+        raise ValueError("frames tensor too small for the batch geometry")
+    return _abi.FrameBatch(frames.data_ptr(), frame_stride, n_frames, width, height, line_length,
+                           layout)
+
+
+class Detector:
+    """Batched HSV-threshold + centroid over frames resident in device memory.
+
+    Owns one library handle (device tables are compiled per range set and
+    cached).  Methods enqueue on `stream` (default: torch's current stream)
+    and do not synchronise.
+    """
+
+    def __init__(self):
+        h = C.c_void_p()
+        p = _default_params(0)
+        rc = _lib.TRIK_VIDTRANSCODE_CV_create(C.byref(p), C.byref(h))
+        if rc != IALG_EOK:
+            raise TrikHsvError(rc, "TRIK_VIDTRANSCODE_CV_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.TRIK_VIDTRANSCODE_CV_delete(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def process_batch(self, frames, width, height, line_length, layout, ranges, *, n_frames=None,
+                      frame_stride=None, stream=None, sums=None, targets=None):
+        """Returns (sums int64 [N,T,3] = points/sumX/sumY, targets int8 [N,T,4] = x/y/size/0)."""
+        import torch
+
+        b = _batch(frames, width, height, line_length, layout, n_frames, frame_stride)
+        arr, T = _ranges(ranges)
+        if sums is None:
+            sums = torch.empty((b.n_frames, T, 3), dtype=torch.int64, device=frames.device)
+        if targets is None:
+            targets = torch.empty((b.n_frames, T, 4), dtype=torch.int8, device=frames.device)
+        rc = _lib.trik_hsv_process_batch(self._h, C.byref(b), arr, T, C.c_void_p(sums.data_ptr()),
+                                         C.c_void_p(targets.data_ptr()), _stream_ptr(stream))
+        if rc:
+            raise TrikHsvError(rc, "trik_hsv_process_batch")
+        return sums, targets
+
+    def batch_sums(self, frames, width, height, line_length, layout, ranges, sums, *,
+                   n_frames=None, frame_stride=None, stream=None):
+        """Hot kernel only; ADDS into `sums` (int64 [N,T,3], caller zeroes it)."""
+        b = _batch(frames, width, height, line_length, layout, n_frames, frame_stride)
+        arr, T = _ranges(ranges)
+        rc = _lib.trik_hsv_batch_sums(self._h, C.byref(b), arr, T, C.c_void_p(sums.data_ptr()),
+                                      _stream_ptr(stream))
+        if rc:
+            raise TrikHsvError(rc, "trik_hsv_batch_sums")
+        return sums
+
+    def batch_masks(self, frames, width, height, line_length, layout, ranges, *, n_frames=None,
+                    frame_stride=None, stream=None):
+        """Verification mode: returns (masks uint8 [N,H,W], sums int64 [N,T,3])."""
+        import torch
+
+        b = _batch(frames, width, height, line_length, layout, n_frames, frame_stride)
+        arr, T = _ranges(ranges)
+        masks = torch.zeros((b.n_frames, height, width), dtype=torch.uint8, device=frames.device)
+        sums = torch.zeros((b.n_frames, T, 3), dtype=torch.int64, device=frames.device)
+        rc = _lib.trik_hsv_batch_masks(self._h, C.byref(b), arr, T, C.c_void_p(masks.data_ptr()),
+                                       C.c_void_p(sums.data_ptr()), _stream_ptr(stream))
+        if rc:
+            raise TrikHsvError(rc, "trik_hsv_batch_masks")
+        return masks, sums
+
+
+def batch_targets(sums, width, height, *, stream=None):
+    """Epilogue only: sums int64 [N,T,3] -> targets int8 [N,T,4]."""
+    import torch
+
+    N, T = sums.shape[0], sums.shape[1]
+    targets = torch.empty((N, T, 4), dtype=torch.int8, device=sums.device)
+    b = _abi.FrameBatch(None, 0, N, width, height, 2 * width, LAYOUT_YUYV)
+    rc = _lib.trik_hsv_batch_targets(C.byref(b), T, C.c_void_p(sums.data_ptr()),
+                                     C.c_void_p(targets.data_ptr()), _stream_ptr(stream))
+    if rc:
+        raise TrikHsvError(rc, "trik_hsv_batch_targets")
+    return targets
+
+
+def synth(frames, width, height, line_length, layout, kind, seed, *, first_frame=0, n_frames=None,
+          frame_stride=None, stream=None):
+    """Fill a uint8 device tensor with synthetic frames (kind 0 uniform, 1 scene)."""
+    b = _batch(frames, width, height, line_length, layout, n_frames, frame_stride)
+    rc = _lib.trik_hsv_synth(C.byref(b), first_frame, kind, seed, _stream_ptr(stream))
+    if rc:
+        raise TrikHsvError(rc, "trik_hsv_synth")
+    return frames
+
+
+# ---------------------------------------------------------------------------
+# ObjectSensor: the codec instance (XDAIS quartet)
+# ---------------------------------------------------------------------------
+def _default_params(num_output_streams=1, fmt_in=FORMAT_YUV422, max_w=640, max_h=480):
+    """TRIK_VIDTRANSCODE_CV_Params defaults (WGLUE:153-184), caps adjustable."""
+    p = _abi.Params()
+    b = p.base
+    b.size = C.sizeof(_abi.Params)
+    b.numOutputStreams = num_output_streams
+    b.formatInput = fmt_in
+    b.formatOutput[0], b.formatOutput[1] = (FORMAT_RGB565X if num_output_streams else FORMAT_UNKNOWN,
+                                            FORMAT_UNKNOWN)
+    b.maxHeightInput, b.maxWidthInput, b.maxFrameRateInput, b.maxBitRateInput = max_h, max_w, 60000, -1
+    b.maxHeightOutput[0], b.maxHeightOutput[1] = max_h, -1
+    b.maxWidthOutput[0], b.maxWidthOutput[1] = max_w, -1
+    b.maxFrameRateOutput[0] = b.maxFrameRateOutput[1] = -1
+    b.maxBitRateOutput[0] = b.maxBitRateOutput[1] = -1
+    b.dataEndianness = 1
+    if num_output_streams == 0:  # caps checks still read index 0
+        b.maxHeightOutput[0], b.maxWidthOutput[0] = max_h, max_w
+    return p
+
+
+def dynamic_params(width, height, line_length, out_width=320, out_height=240, out_line_length=640):
+    d = _abi.DynamicParams()
+    d.base.size = C.sizeof(_abi.DynamicParams)
+    d.base.keepInputResolutionFlag[1] = 1
+    d.base.outputHeight[0], d.base.outputWidth[0] = out_height, out_width
+    d.base.keepInputFrameRateFlag[0] = d.base.keepInputFrameRateFlag[1] = 1
+    d.base.inputFrameRate = -1
+    d.base.forceFrame[0] = d.base.forceFrame[1] = -1
+    d.inputHeight, d.inputWidth, d.inputLineLength = height, width, line_length
+    d.outputLineLength[0], d.outputLineLength[1] = out_line_length, -1
+    return d
+
+
+class ObjectSensor:
+    """One TRIK_VIDTRANSCODE_CV codec instance (vidtranscode_cv_fxns.c)."""
+
+    def __init__(self, params: _abi.Params | None = None):
+        h = C.c_void_p()
+        rc = _lib.TRIK_VIDTRANSCODE_CV_create(C.byref(params) if params is not None else None,
+                                              C.byref(h))
+        if rc != IALG_EOK:
+            raise TrikHsvError(rc, "TRIK_VIDTRANSCODE_CV_create")
+        self._h = h
+        self.params = params if params is not None else _default_params(1)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.TRIK_VIDTRANSCODE_CV_delete(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def control(self, cmd: int, dyn: _abi.DynamicParams | None = None,
+                status: _abi.Status | None = None):
+        st = status if status is not None else _abi.Status()
+        rc = _lib.TRIK_VIDTRANSCODE_CV_control(self._h, cmd, C.byref(dyn) if dyn is not None else None,
+                                               C.byref(st))
+        return rc, st
+
+    def set_params(self, width, height, line_length, **kw) -> int:
+        rc, _ = self.control(XDM_SETPARAMS, dynamic_params(width, height, line_length, **kw))
+        return rc
+
+    def process(self, frame, hsv_range: Sequence[int], out_buffer=None, auto_detect=False,
+                num_bytes=None, input_id=0):
+        """One host frame (bytes / numpy uint8) -> (rc, OutArgs)."""
+        import numpy as np
+
+        fr = np.ascontiguousarray(np.frombuffer(frame, np.uint8) if isinstance(frame, (bytes, bytearray))
+                                  else frame, dtype=np.uint8)
+        ib = _abi.BufDesc1()
+        ib.numBufs = 1
+        ib.descs[0].buf = fr.ctypes.data
+        ib.descs[0].bufSize = fr.size
+        ob = _abi.BufDesc()
+        keep = []
+        if out_buffer is not None:
+            ob_arr = (C.c_void_p * 1)(out_buffer.ctypes.data)
+            sz_arr = (C.c_int32 * 1)(out_buffer.nbytes)
+            keep += [ob_arr, sz_arr]
+            ob.bufs, ob.numBufs, ob.bufSizes = ob_arr, 1, sz_arr
+        ia = _abi.InArgs()
+        ia.base.size = C.sizeof(_abi.InArgs)
+        ia.base.numBytes = fr.size if num_bytes is None else num_bytes
+        ia.base.inputID = input_id
+        ia.alg = _abi.InArgsAlg(*[int(v) for v in hsv_range[:6]], int(bool(auto_detect)))
+        oa = _abi.OutArgs()
+        oa.base.size = C.sizeof(_abi.OutArgs)
+        rc = _lib.TRIK_VIDTRANSCODE_CV_process(self._h, C.byref(ib), C.byref(ob), C.byref(ia),
+                                               C.byref(oa))
+        return rc, oa
