@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--targets", type=int, default=4)
     ap.add_argument("--kind", type=int, default=0, help="0 uniform random bytes, 1 scene")
-    ap.add_argument("--cpu-frames", type=int, default=512, help="CPU baseline sample (frames)")
+    ap.add_argument("--cpu-frames", type=int, default=1024, help="CPU baseline sample (frames)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="rocprofv3 FETCH_SIZE summary used for roofline.traffic")

@@ -466,8 +466,10 @@ extern "C" int32_t trik_hsv_batch_sums(TRIK_VIDTRANSCODE_CV_Handle h, const Trik
 extern "C" int32_t trik_hsv_batch_targets(const TrikHsvFrameBatch* b, int32_t n,
                                           const TrikHsvTargetSums* sums, TrikHsvTarget* targets,
                                           void* stream) {
-  const std::string e = validate_batch(b);
-  if (!e.empty()) return fail(TRIK_IVIDTRANSCODE_EFAIL, e);
+  // only the geometry matters here (no frame bytes are read)
+  if (!b) return fail(TRIK_IVIDTRANSCODE_EFAIL, "batch is NULL");
+  if (b->n_frames < 0 || b->width <= 0 || b->height <= 0 || b->width > 32767 || b->height > 32767)
+    return fail(TRIK_IVIDTRANSCODE_EFAIL, "batch_targets: need n_frames >= 0 and 0 < width, height <= 32767");
   if (n < 1 || n > TRIK_HSV_MAX_RANGES) return fail(TRIK_IVIDTRANSCODE_EFAIL, "n_ranges must be 1..64");
   if (b->n_frames > 0 && (!sums || !targets)) return fail(TRIK_IVIDTRANSCODE_EFAIL, "NULL buffer");
   HIP_TRY(launch_targets(*b, n, sums, targets, static_cast<hipStream_t>(stream)));
