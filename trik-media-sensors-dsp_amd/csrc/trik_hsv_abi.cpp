@@ -108,6 +108,8 @@ struct TrikCvHandle {
   int table_groups_cap = 0;
   std::vector<uint32_t> table_key;
   RangeTables* h_tables = nullptr;  // pinned staging
+  StripeTables* d_stripe = nullptr;
+  StripeTables* h_stripe = nullptr;
   hipEvent_t tables_busy = nullptr;
 
   // process() staging
@@ -129,6 +131,8 @@ void release(TrikCvHandle* h) {
   if (h->tables_busy) (void)hipEventSynchronize(h->tables_busy);
   (void)hipFree(h->d_tables);
   (void)hipHostFree(h->h_tables);
+  (void)hipFree(h->d_stripe);
+  (void)hipHostFree(h->h_stripe);
   (void)hipFree(h->d_frame);
   (void)hipFree(h->d_sums);
   (void)hipFree(h->d_targets);
@@ -205,16 +209,24 @@ int32_t ensure_tables(TrikCvHandle* h, const TRIK_VIDTRANSCODE_CV_InArgsAlg* ran
   if (groups > h->table_groups_cap) {
     (void)hipFree(h->d_tables);
     (void)hipHostFree(h->h_tables);
+    (void)hipFree(h->d_stripe);
+    (void)hipHostFree(h->h_stripe);
     h->d_tables = nullptr; h->h_tables = nullptr; h->table_groups_cap = 0;
+    h->d_stripe = nullptr; h->h_stripe = nullptr;
     HIP_TRY(hipMalloc(&h->d_tables, sizeof(RangeTables) * groups));
     HIP_TRY(hipHostMalloc(&h->h_tables, sizeof(RangeTables) * groups, hipHostMallocDefault));
+    HIP_TRY(hipMalloc(&h->d_stripe, sizeof(StripeTables) * groups));
+    HIP_TRY(hipHostMalloc(&h->h_stripe, sizeof(StripeTables) * groups, hipHostMallocDefault));
     h->table_groups_cap = groups;
   }
   for (int g = 0; g < groups; ++g) {
     const int cnt = n - g * kRangesPerLaunch < kRangesPerLaunch ? n - g * kRangesPerLaunch : kRangesPerLaunch;
     compile_tables(ranges + g * kRangesPerLaunch, cnt, &h->h_tables[g]);
+    compile_stripe_tables(h->h_tables[g], cnt, &h->h_stripe[g]);
   }
   HIP_TRY(hipMemcpyAsync(h->d_tables, h->h_tables, sizeof(RangeTables) * groups,
+                         hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(h->d_stripe, h->h_stripe, sizeof(StripeTables) * groups,
                          hipMemcpyHostToDevice, s));
   h->table_key.swap(key);
   return 0;
@@ -237,10 +249,17 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
     a.range_offset = g * kRangesPerLaunch;
     a.sums_ranges = n;
     a.tables = h->d_tables + g;
+    a.stripe_tables = h->d_stripe + g;
     a.sums = sums;
     a.masks = masks;
     a.mask_shift = g * kRangesPerLaunch;
-    HIP_TRY(launch_reduce(a, masks != nullptr, s));
+    // the stripe kernel is the hot path; the generic kernel takes misaligned
+    // inputs and rows wider than 8192 pixels
+    const int e = launch_stripe(a, masks != nullptr, s);
+    if (e == hipErrorNotSupported)
+      HIP_TRY(launch_reduce(a, masks != nullptr, s));
+    else
+      HIP_TRY(e);
   }
   if (!h->tables_busy) HIP_TRY(hipEventCreateWithFlags(&h->tables_busy, hipEventDisableTiming));
   HIP_TRY(hipEventRecord(h->tables_busy, s));

@@ -32,8 +32,25 @@ struct PackedRange {
   uint32_t from, to, expect;
 };
 
+// Tables of the stripe kernel (trik_hsv_stripe.hip), staged in LDS.  Layout
+// chosen for LDS banking: the two small tables are
+// replicated once per bank so a wave's random lookups are conflict-free, the
+// large one has rows padded to 260 bytes so the bank rotates with mx.
+//   sv[mx * 260 + mn]        : T-bit (sat AND val) mask for max mx, min mn
+//   m43[d][32]               : s_mult43_div, one copy per bank (dwords)
+//   hue[H][32]               : byte-spread hue mask (range t -> bit 8t), per bank
+constexpr int kSvStride = 260;
+constexpr int kBanks = 32;
+struct alignas(16) StripeTables {
+  uint8_t sv[256 * kSvStride];
+  uint32_t m43[256 * kBanks];
+  uint32_t hue[256 * kBanks];
+};
+static_assert(sizeof(StripeTables) == 66560 + 32768 + 32768, "table layout");
+
 PackedRange pack_range(const TRIK_VIDTRANSCODE_CV_InArgsAlg& r);
 void compile_tables(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTables* out);
+void compile_stripe_tables(const RangeTables& base, int n, StripeTables* out);
 
 struct KernelArgs {
   const uint8_t* frames;
@@ -45,6 +62,7 @@ struct KernelArgs {
   int32_t range_offset;  // index of this launch's first range in the sums array
   int32_t sums_ranges;   // ranges per frame in the sums array (row pitch)
   const RangeTables* tables;
+  const StripeTables* stripe_tables;
   TrikHsvTargetSums* sums;
   uint8_t* masks;        // verification mode only
   int32_t mask_shift;    // bit position of this launch's range 0 in the mask byte
@@ -52,6 +70,9 @@ struct KernelArgs {
 
 // Launchers (trik_hsv_kernels.hip).  Return hipError_t as int.
 int launch_reduce(const KernelArgs& a, bool write_masks, hipStream_t s);
+// The optimised hot kernel (trik_hsv_stripe.hip); returns hipErrorNotSupported
+// when the geometry needs the generic kernel (misaligned input, width > 8192).
+int launch_stripe(const KernelArgs& a, bool write_masks, hipStream_t s);
 int launch_targets(const TrikHsvFrameBatch& b, int n_ranges, const TrikHsvTargetSums* sums,
                    TrikHsvTarget* targets, hipStream_t s);
 int launch_synth(const TrikHsvFrameBatch& b, uint8_t* frames, int first_frame, int kind,

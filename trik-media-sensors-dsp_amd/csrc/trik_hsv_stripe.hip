@@ -1,0 +1,340 @@
+// trik_hsv_stripe.hip -- the optimised hot kernel for gfx950.
+//
+// One read-once pass over N frames fusing the reference's two loops
+// (WSEQ:251-284 convert, WSEQ:316-354 threshold + centroid; WSEQ/OSEQ as in
+// include/trik_hsv.h) for up to 4 HSV ranges.  Design:
+//
+//  * Column stripes.  A workgroup of B <= 1024 threads covers k = 1024/cpr
+//    rows of cpr 16-byte chunks (8 pixels each); lane t owns chunk column
+//    t % cpr for the whole tile and walks rows t / cpr, +k, +2k, ...  Loads are
+//    coalesced dwordx4 (YUYV) or 2 x dwordx2 (ov7670 planes), the next row's
+//    chunk prefetched while the current one computes.
+//  * Per pixel, branch-free: YUV -> RGB presums with v_dot4_u32_u8, clamp via
+//    v_bfe_i32 + v_med3_i32 (the 16-bit wrap of _add2 falls out of bfe),
+//    max3/min3, the hue case select as v_cndmask, h = m*diff + base as
+//    v_mad_i32_i24, then two LDS lookups: sat&val mask by (max,min) and the
+//    byte-spread (hue & sv) mask by (H, sv).  No per-range work per pixel.
+//  * Accumulation with fixed columns needs no per-pixel x weight: per lane,
+//    pairs of pixels add into byte-packed counters with v_add3_u32 (range t in
+//    byte t), odd pixels into one more counter, and a prefix-of-prefix counter
+//    gives the sum over rows of y * count.  About one VALU op
+//    per pixel; unpacked to 32-bit per range once per tile.
+//  * Per tile: DPP wave reduction, one 64-bit atomic per value per wave.
+#include <hip/hip_runtime.h>
+
+#include "trik_hsv_internal.h"
+
+namespace trik_hsv {
+
+namespace {
+
+constexpr int kMaxBlock = 1024;
+constexpr int kMaxSteps = 31;  // byte counters: P_i <= 2*31, sum of four <= 248
+constexpr int kQFlush = 7;     // steps per Q block: block-relative sums <= 8*(1+...+7) = 224
+
+struct StripeGeom {
+  int32_t cpr;              // 16-byte chunks per row (width / 8)
+  int32_t k;                // rows per step
+  int32_t steps;            // steps per tile (<= kMaxSteps)
+  int32_t tiles_per_frame;
+  int64_t n_tiles;
+};
+
+__device__ __forceinline__ int clamp8_shift6(uint32_t s) {
+  // bits 6..15 of the presum, sign-extended from bit 15: (int16)s >> 6.
+  const int v = ((int)(s << 16)) >> 22;
+  return min(max(v, 0), 255);
+}
+
+// YUYV word w (b0=Y0, b1=U, b2=Y1, b3=V) -> byte-spread detection masks of its
+// two pixels.  wc = w ^ 0xFF00FF00 (complemented chroma for the negative G
+// weights of WSEQ:188-190 on an unsigned dot product).
+// bank4 = 4 * (lane & 31): this lane's copy in the per-bank replicated tables
+template <int PIX>
+__device__ __forceinline__ uint32_t detect(uint32_t w, uint32_t wc, const uint8_t* lds,
+                                           uint32_t m43_lane, uint32_t hue_lane) {
+  // presums of WSEQ:183-201
+  constexpr uint32_t kY = PIX == 0 ? 74u : (74u << 16);
+  const uint32_t sR = __builtin_amdgcn_udot4(w, kY | (102u << 24), (uint32_t)-14248, false);
+  const uint32_t sG = __builtin_amdgcn_udot4(wc, kY | (25u << 8) | (52u << 24), (uint32_t)-10939, false);
+  const uint32_t sB = __builtin_amdgcn_udot4(w, kY | (129u << 8), (uint32_t)-17672, false);
+  const int r = clamp8_shift6(sR), g = clamp8_shift6(sG), b = clamp8_shift6(sB);
+  // WSEQ:207-249: max/min, LUT43[delta], hue case G > B > R on ties
+  const int mx = max(r, max(g, b));
+  const int mn = min(r, min(g, b));
+  const int m = (int)*reinterpret_cast<const uint32_t*>(lds + (((uint32_t)(mx - mn) << 7) + m43_lane));
+  const int dR = g - b, dG = b - r, dB = r - g;
+  const bool eqG = mx == g, eqB = mx == b;
+  int diff = eqB ? dB : dR;
+  diff = eqG ? dG : diff;
+  int base = eqB ? 43690 : 0;
+  base = eqG ? 21845 : base;
+  const uint32_t h = (uint32_t)(__mul24(m, diff) + base);  // m < 2^14, |diff| < 2^8
+  const uint32_t H = (h >> 8) & 0xFFu;
+  const uint32_t hue = *reinterpret_cast<const uint32_t*>(lds + ((H << 7) + hue_lane));
+  const uint32_t sv = lds[__mul24(mx, kSvStride) + mn];
+  // spread sv's bit t to bit 8t: terms at t + 7s are disjoint for t, s < 4
+  return hue & __mul24(sv, 0x00204081u);
+}
+
+// Sum each of N values over the 64 lanes of the wave (result valid in lane
+// 63).  DPP row_shr 1,2,4,8 builds row prefixes, row_bcast15/31 folds rows.
+// The N reductions are interleaved so independent DPP ops hide each other's
+// hazards.
+template <int N>
+__device__ __forceinline__ void wave_sums(uint32_t (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x111, 0xF, 0xF, true);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x112, 0xF, 0xF, true);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x114, 0xF, 0xF, true);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x118, 0xF, 0xF, true);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x142, 0xA, 0xF, false);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x143, 0xC, 0xF, false);
+}
+
+// Wave-reduce the per-lane frame accumulators and add them to sums[frame].
+template <int NR>
+__device__ __forceinline__ void flush_frame(uint32_t (&acc)[3 * NR], int frame, const KernelArgs& a) {
+  wave_sums<3 * NR>(acc);
+  if ((threadIdx.x & 63) == 63) {
+    TrikHsvTargetSums* dst = a.sums + (int64_t)frame * a.sums_ranges + a.range_offset;
+#pragma unroll
+    for (int v = 0; v < 3 * NR; ++v)
+      if (acc[v])
+        atomicAdd(reinterpret_cast<unsigned long long*>(&dst[v / 3].points) + (v % 3),
+                  (unsigned long long)acc[v]);
+  }
+#pragma unroll
+  for (int v = 0; v < 3 * NR; ++v) acc[v] = 0;
+}
+
+template <int LAYOUT>
+__device__ __forceinline__ void load_chunk(const uint8_t* p, int64_t plane, uint32_t w[4]) {
+  if (LAYOUT == TRIK_HSV_LAYOUT_YUYV) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+  } else {
+    const uint2 vy = *reinterpret_cast<const uint2*>(p);
+    const uint2 vc = *reinterpret_cast<const uint2*>(p + plane);
+    // OSEQ:369-373: U = odd chroma byte, V = even chroma byte
+    w[0] = __builtin_amdgcn_perm(vc.x, vy.x, 0x04010500u);
+    w[1] = __builtin_amdgcn_perm(vc.x, vy.x, 0x06030702u);
+    w[2] = __builtin_amdgcn_perm(vc.y, vy.y, 0x04010500u);
+    w[3] = __builtin_amdgcn_perm(vc.y, vy.y, 0x06030702u);
+  }
+}
+
+// byte-spread mask -> bit mask (range t -> bit t)
+__device__ __forceinline__ uint32_t pack_bits(uint32_t e) {
+  return ((e * 0x01020408u) >> 24) & 0xFu;  // bit 8t lands on bit 24+t
+}
+
+template <int LAYOUT, int NR, bool MASKS>
+__global__ __launch_bounds__(kMaxBlock) void stripe_kernel(KernelArgs a, StripeGeom g) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(a.stripe_tables);
+    uint4* dst = reinterpret_cast<uint4*>(lds);
+    for (int i = threadIdx.x; i < (int)(sizeof(StripeTables) / 16); i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+
+  const int t = threadIdx.x;
+  const uint32_t m43_lane = (uint32_t)offsetof(StripeTables, m43) + ((t & 31) << 2);
+  const uint32_t hue_lane = (uint32_t)offsetof(StripeTables, hue) + ((t & 31) << 2);
+  const bool active = t < g.k * g.cpr;
+  const int col = active ? t % g.cpr : 0;
+  const int ro = active ? t / g.cpr : 0;
+  const int64_t plane = (int64_t)a.height * a.line_length;
+  const int64_t rowstep = (int64_t)g.k * a.line_length;
+  const int col_bytes = LAYOUT == TRIK_HSV_LAYOUT_YUYV ? col * 16 : col * 8;
+  const uint32_t x0 = (uint32_t)col * 8;
+
+  const int64_t t_begin = g.n_tiles * blockIdx.x / gridDim.x;
+  const int64_t t_end = g.n_tiles * (blockIdx.x + 1) / gridDim.x;
+  // per-lane 32-bit sums of the current frame: {N, sumX, sumY} per range
+  uint32_t acc[3 * NR];
+#pragma unroll
+  for (int v = 0; v < 3 * NR; ++v) acc[v] = 0;
+  int cur = t_begin < t_end ? (int)(t_begin / g.tiles_per_frame) : -1;
+  for (int64_t tile = t_begin; tile < t_end; ++tile) {
+    const int f = (int)(tile / g.tiles_per_frame);
+    if (f != cur) {  // uniform across the workgroup
+      flush_frame<NR>(acc, cur, a);
+      cur = f;
+    }
+    const int r0 = (int)(tile - (int64_t)f * g.tiles_per_frame) * g.k * g.steps;
+    const int y0 = r0 + ro;
+    // steps that hold at least one valid row of this tile (uniform per block)
+    const int steps = min(g.steps, (a.height - r0 + g.k - 1) / g.k);
+    const uint8_t* p = a.frames + (int64_t)f * a.frame_stride + (int64_t)y0 * a.line_length + col_bytes;
+
+    // Byte-packed per-lane counters (range t in byte t):
+    //   P_i : pixels 2i and 2i+1 of the chunk    O : odd pixels
+    //   Q   : sum over the current block of steps of (cumulative count - CumS),
+    //         CumS = cumulative count at the block start.  Q's byte fields may
+    //         carry into each other while adding; the block-end value
+    //         Q - nb*CumS has true fields in [0, 224], and packed arithmetic
+    //         is exact mod 2^32, so the fields come out right.
+    //   Qa/Qb, Ba/Bb : 16-bit fields (ranges 0,2 / 1,3) collecting, per block,
+    //         the sums above and nb*CumS.
+    uint32_t P0 = 0, P1 = 0, P2 = 0, P3 = 0, O = 0, Q = 0, CumS = 0;
+    uint32_t Qa = 0, Qb = 0, Ba = 0, Bb = 0;
+    int nb = 0;
+    // Software pipeline, two rows ahead.  Loads are unconditional (a row past
+    // the frame end re-reads the tile's first row) so the compiler can wait
+    // with a counted vmcnt instead of draining every load each step.
+    const uint8_t* pf = active ? p : a.frames + (int64_t)f * a.frame_stride;
+    const int vsteps = active ? min(steps, (a.height - y0 + g.k - 1) / g.k) : 0;  // valid steps, this lane
+    // one step: 8 pixels of row y0 + s*k from the chunk words in `cw`
+    auto step = [&](const uint32_t (&cw)[4], int s) {
+      const bool valid = s < vsteps;
+      uint32_t e[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t wc = cw[q] ^ 0xFF00FF00u;
+        e[2 * q] = detect<0>(cw[q], wc, lds, m43_lane, hue_lane);
+        e[2 * q + 1] = detect<1>(cw[q], wc, lds, m43_lane, hue_lane);
+      }
+      if (MASKS && valid) {
+        const int y = y0 + s * g.k;
+        uint8_t* mp = a.masks + ((int64_t)f * a.height + y) * a.width + x0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint8_t bits = (uint8_t)(pack_bits(e[j]) << a.mask_shift);
+          mp[j] = a.mask_shift ? (uint8_t)(mp[j] | bits) : bits;
+        }
+      }
+      if (valid) {  // false only for rows past the frame end and idle lanes
+        P0 = P0 + e[0] + e[1];
+        P1 = P1 + e[2] + e[3];
+        P2 = P2 + e[4] + e[5];
+        P3 = P3 + e[6] + e[7];
+        O = O + e[1] + e[3];
+        O = O + e[5] + e[7];
+      }
+      Q = Q + P0 + P1;
+      Q = Q + P2 + P3;
+      ++nb;
+      if (nb == kQFlush || s + 1 == steps) {  // uniform across the block
+        const uint32_t T = Q - (uint32_t)nb * CumS;
+        Qa += T & 0x00FF00FFu;
+        Qb += (T >> 8) & 0x00FF00FFu;
+        Ba += (uint32_t)nb * (CumS & 0x00FF00FFu);
+        Bb += (uint32_t)nb * ((CumS >> 8) & 0x00FF00FFu);
+        CumS = P0 + P1 + P2 + P3;
+        Q = 0;
+        nb = 0;
+      }
+    };
+    auto row_ptr = [&](int s) { return s < vsteps ? pf + (int64_t)s * rowstep : pf; };
+    // three buffers rotate statically (unroll by 3): two rows stay in flight
+    uint32_t wa[4], wb[4], wc3[4];
+    load_chunk<LAYOUT>(row_ptr(0), plane, wa);
+    load_chunk<LAYOUT>(row_ptr(1), plane, wb);
+    for (int s = 0; s < steps; s += 3) {
+      load_chunk<LAYOUT>(row_ptr(s + 2), plane, wc3);
+      step(wa, s);
+      if (s + 1 >= steps) break;
+      load_chunk<LAYOUT>(row_ptr(s + 3), plane, wa);
+      step(wb, s + 1);
+      if (s + 2 >= steps) break;
+      load_chunk<LAYOUT>(row_ptr(s + 4), plane, wb);
+      step(wc3, s + 2);
+    }
+    Qa += Ba;  // sum over steps of the cumulative count, 16-bit fields
+    Qb += Bb;
+
+    // unpack per range into the frame accumulators
+    const uint32_t C = P0 + P1 + P2 + P3;
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) {
+      const int sh = 8 * rr;
+      const uint32_t c = (C >> sh) & 0xFFu;
+      const uint32_t wx = 2u * ((P1 >> sh) & 0xFFu) + 4u * ((P2 >> sh) & 0xFFu) +
+                          6u * ((P3 >> sh) & 0xFFu) + ((O >> sh) & 0xFFu);
+      const uint32_t qq = ((rr & 1) ? (Qb >> ((rr >> 1) * 16)) : (Qa >> ((rr >> 1) * 16))) & 0xFFFFu;
+      acc[3 * rr + 0] += c;
+      acc[3 * rr + 1] += x0 * c + wx;
+      // sum over steps of (y0 + k*s) * c_s = y0*C + k*(steps*C - sum of prefix counts)
+      acc[3 * rr + 2] += (uint32_t)y0 * c + (uint32_t)g.k * ((uint32_t)steps * c - qq);
+    }
+  }
+  if (cur >= 0) flush_frame<NR>(acc, cur, a);
+}
+
+bool geometry(const KernelArgs& a, StripeGeom& g) {
+  const int cpr = a.width >> 3;
+  if (cpr <= 0 || cpr > kMaxBlock || a.height <= 0) return false;
+  const int k = kMaxBlock / cpr;
+  const int steps_total = (a.height + k - 1) / k;
+  const int tiles = (steps_total + kMaxSteps - 1) / kMaxSteps;
+  g.cpr = cpr;
+  g.k = k;
+  g.tiles_per_frame = tiles;
+  g.steps = (steps_total + tiles - 1) / tiles;
+  g.n_tiles = (int64_t)tiles * a.n_frames;
+  return true;
+}
+
+int cu_count_stripe() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+    return 256;
+  return n;
+}
+
+template <int LAYOUT, int NR, bool MASKS>
+int launch_t(const KernelArgs& a, const StripeGeom& g, hipStream_t s) {
+  auto kern = stripe_kernel<LAYOUT, NR, MASKS>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)sizeof(StripeTables));
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  static int cus = 0;
+  if (!cus) cus = cu_count_stripe();
+  const int block = ((g.k * g.cpr + 63) / 64) * 64;
+  const int64_t grid = g.n_tiles < cus ? g.n_tiles : cus;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(block), sizeof(StripeTables), s, a, g);
+  return hipGetLastError();
+}
+
+template <int LAYOUT, bool MASKS>
+int launch_nr(const KernelArgs& a, const StripeGeom& g, hipStream_t s) {
+  switch (a.n_ranges) {
+    case 1: return launch_t<LAYOUT, 1, MASKS>(a, g, s);
+    case 2: return launch_t<LAYOUT, 2, MASKS>(a, g, s);
+    case 3: return launch_t<LAYOUT, 3, MASKS>(a, g, s);
+    case 4: return launch_t<LAYOUT, 4, MASKS>(a, g, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+int launch_stripe(const KernelArgs& a, bool write_masks, hipStream_t s) {
+  StripeGeom g;
+  if (!geometry(a, g)) return hipErrorNotSupported;
+  const int64_t need = a.layout == TRIK_HSV_LAYOUT_YUYV ? 16 : 8;
+  if ((reinterpret_cast<uintptr_t>(a.frames) % need) || (a.frame_stride % need) ||
+      (a.line_length % need))
+    return hipErrorNotSupported;
+  if (g.n_tiles == 0) return hipSuccess;
+  if (a.layout == TRIK_HSV_LAYOUT_YUYV)
+    return write_masks ? launch_nr<TRIK_HSV_LAYOUT_YUYV, true>(a, g, s)
+                       : launch_nr<TRIK_HSV_LAYOUT_YUYV, false>(a, g, s);
+  return write_masks ? launch_nr<TRIK_HSV_LAYOUT_OV7670, true>(a, g, s)
+                     : launch_nr<TRIK_HSV_LAYOUT_OV7670, false>(a, g, s);
+}
+
+}  // namespace trik_hsv

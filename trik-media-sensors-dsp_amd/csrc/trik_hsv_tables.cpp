@@ -67,4 +67,19 @@ void compile_tables(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTa
   }
 }
 
+void compile_stripe_tables(const RangeTables& base, int n, StripeTables* out) {
+  memset(out, 0, sizeof(*out));
+  const uint8_t keep = (uint8_t)((1u << (n < 4 ? n : 4)) - 1u);
+  for (int mx = 0; mx < 256; ++mx)
+    for (int mn = 0; mn < 256; ++mn) out->sv[mx * kSvStride + mn] = base.sv[mx * 256 + mn] & keep;
+  for (int i = 0; i < 256; ++i) {
+    uint32_t spread = 0;
+    for (int t = 0; t < n && t < 4; ++t) spread |= ((uint32_t)(base.hue[i] >> t) & 1u) << (8 * t);
+    for (int b = 0; b < kBanks; ++b) {
+      out->m43[i * kBanks + b] = base.lut43[i];
+      out->hue[i * kBanks + b] = spread;
+    }
+  }
+}
+
 }  // namespace trik_hsv
