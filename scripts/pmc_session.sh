@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 OUT="$GRAFT_REPO_ROOT/gpurun_out"
 TAG="${1:-pmc}"
 shift || true
-ARGS="${*:---frames 1024 --steps 5 --warmup 2 --no-cpu-baseline}"
+ARGS="${*:---steps 3 --warmup 1 --no-cpu-baseline}"
 mkdir -p "$OUT/$TAG"
 cd /tmp && export TMPDIR=/tmp
 i=0

@@ -95,31 +95,30 @@ DEF(k2_andimm, "v_and_b32 %0, 0xff00, %0\n v_xor_b32 %0, %0, %1")
 DEF(k2_addimm, "v_add_u32 %0, 0x1234, %0\n v_xor_b32 %0, %0, %1")
 DEF(k2_not, "v_not_b32 %0, %0\n v_xor_b32 %0, %0, %1")
 
+DEF(k3_pkmad, "v_pk_mad_u16 %0, %0, %1, %0")
+DEF(k3_subclamp, "v_sub_u16 %0, %0, %1 clamp")
+DEF(k3_or3, "v_or3_b32 %0, %0, %1, %0")
+DEF(k3_lshlor, "v_lshl_or_b32 %0, %0, 3, %1")
+DEF(k3_addu24, "v_mad_u32_u24 %0, %0, %1, %0")
+DEF(k3_mulhi16, "v_mul_hi_u32_u24 %0, %0, %1")
+DEF(k3_addc, "v_add_u32 %0, 0xff00ff, %0\n v_xor_b32 %0, %0, %1")
+DEF(k3_subb16, "v_subrev_u16 %0, %0, %1")
+DEF(k3_cvtu16, "v_cvt_f32_ubyte0 %0, %0\n v_xor_b32 %0, %0, %1")
+
 typedef void (*K)(uint32_t*, uint32_t);
 struct T { const char* name; K k; int instrs_per_step; };
 
 int main() {
-  T tests[] = {{"v_add_u32", k_add, 1}, {"v_xor_b32", k_xor, 1}, {"v_dot4_u32_u8", k_dot4, 1},
-               {"v_max_i16", k2_maxi16, 1},
-               {"v_min_i16", k2_mini16, 1},
-               {"v_min_u16", k2_minu16, 1},
-               {"v_ashrrev_i16", k2_ashr16, 1},
-               {"v_lshrrev_b16", k2_lshr16, 1},
-               {"v_lshlrev_b16", k2_lshl16, 1},
-               {"v_add_u16", k2_add16, 1},
-               {"v_mul_lo_u16", k2_mul16, 1},
-               {"v_mad_u16", k2_mad16, 1},
-               {"v_cmp_eq_u32+xor", k2_cmpeq, 2},
-               {"v_cmp_eq_u16+xor", k2_cmpeq16, 2},
-               {"v_cndmask_b32_e32", k2_cnde32, 1},
-               {"v_med3_u16", k2_med3u16, 1},
-               {"v_med3_i16", k2_med3i16, 1},
-               {"v_lshlrev_b32", k2_lshlrev, 1},
-               {"v_max3_u32", k2_max3u, 1},
-               {"v_subrev_u32", k2_subrev, 1},
-               {"v_and_b32+xor", k2_andimm, 2},
-               {"v_add_u32+xor", k2_addimm, 2},
-               {"v_not_b32+xor", k2_not, 2}};
+  T tests[] = {{"v_add_u32", k_add, 1}, {"v_dot4_u32_u8", k_dot4, 1}, {"v_cndmask sgpr", k_cnds, 1}, {"v_cmp+cndmask", k_cndmask, 2},
+               {"v_pk_mad_u16", k3_pkmad, 1},
+               {"v_sub_u16 clamp", k3_subclamp, 1},
+               {"v_or3_b32", k3_or3, 1},
+               {"v_lshl_or_b32", k3_lshlor, 1},
+               {"v_mad_u32_u24", k3_addu24, 1},
+               {"v_mul_hi_u32_u24", k3_mulhi16, 1},
+               {"v_add_u32+xor", k3_addc, 2},
+               {"v_subrev_u16", k3_subb16, 1},
+               {"v_cvt_f32_ubyte0+xor", k3_cvtu16, 2}};
   int dev = 0, cus = 0, clk = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   hipDeviceGetAttribute(&clk, hipDeviceAttributeClockRate, dev);

@@ -33,20 +33,25 @@ struct PackedRange {
 };
 
 // Tables of the stripe kernel (trik_hsv_stripe.hip), staged in LDS.  Layout
-// chosen for LDS banking: the two small tables are
-// replicated once per bank so a wave's random lookups are conflict-free, the
-// large one has rows padded to 260 bytes so the bank rotates with mx.
-//   sv[mx * 260 + mn]        : T-bit (sat AND val) mask for max mx, min mn
-//   m43[d][32]               : s_mult43_div, one copy per bank (dwords)
-//   hue[H][32]               : byte-spread hue mask (range t -> bit 8t), per bank
+// chosen for LDS banking and cheap addressing: the two
+// small tables are replicated once per bank so a wave's random lookups are
+// conflict-free, interleaved in 256-byte rows so that both addresses are one
+// and/or of a value already in the high byte; the large table has rows padded
+// to 260 bytes so the bank rotates with mx.
+//   sv[mx * 260 + mn] : T-bit (sat AND val) mask for max mx, min mn (offset 0,
+//                       so its address is one v_mad_u32_u24)
+//   row[i] = { hue[i] x 32 banks, m43[i] x 32 banks }   (dwords)
+//     hue[H] : byte-spread hue mask (range t -> bit 8t)
+//     m43[d] : s_mult43_div (WSEQ:389-407)
 constexpr int kSvStride = 260;
 constexpr int kBanks = 32;
 struct alignas(16) StripeTables {
   uint8_t sv[256 * kSvStride];
-  uint32_t m43[256 * kBanks];
-  uint32_t hue[256 * kBanks];
+  uint32_t rows[256][2 * kBanks];
 };
-static_assert(sizeof(StripeTables) == 66560 + 32768 + 32768, "table layout");
+static_assert(sizeof(StripeTables) == 66560 + 65536, "table layout");
+constexpr uint32_t kHueRowOffset = 0;    // bytes into a row
+constexpr uint32_t kM43RowOffset = 128;
 
 PackedRange pack_range(const TRIK_VIDTRANSCODE_CV_InArgsAlg& r);
 void compile_tables(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTables* out);

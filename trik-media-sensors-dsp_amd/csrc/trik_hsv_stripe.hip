@@ -9,11 +9,14 @@
 //    t % cpr for the whole tile and walks rows t / cpr, +k, +2k, ...  Loads are
 //    coalesced dwordx4 (YUYV) or 2 x dwordx2 (ov7670 planes), the next row's
 //    chunk prefetched while the current one computes.
-//  * Per pixel, branch-free: YUV -> RGB presums with v_dot4_u32_u8, clamp via
-//    v_bfe_i32 + v_med3_i32 (the 16-bit wrap of _add2 falls out of bfe),
-//    max3/min3, the hue case select as v_cndmask, h = m*diff + base as
-//    v_mad_i32_i24, then two LDS lookups: sat&val mask by (max,min) and the
-//    byte-spread (hue & sv) mask by (H, sv).  No per-range work per pixel.
+//  * Per pixel, branch-free, ~30 VALU ops: YUV -> RGB presums with
+//    v_dot4_u32_u8, clamp via v_bfe_i32 + v_med3_i32 (the 16-bit wrap of
+//    _add2 falls out of bfe), max3/min3, the hue case select as v_cndmask,
+//    h = m*diff + base as v_mad_i32_i24, and three LDS lookups: LUT43 and the
+//    sat&val mask by (max, min), then the byte-spread hue mask by H.  A step's
+//    8 pixels issue their first two lookups before any hue index is formed,
+//    so LDS latency overlaps (4 waves/SIMD cannot hide it otherwise).  No
+//    per-range work per pixel.
 //  * Accumulation with fixed columns needs no per-pixel x weight: per lane,
 //    pairs of pixels add into byte-packed counters with v_add3_u32 (range t in
 //    byte t), odd pixels into one more counter, and a prefix-of-prefix counter
@@ -40,41 +43,71 @@ struct StripeGeom {
   int64_t n_tiles;
 };
 
-__device__ __forceinline__ int clamp8_shift6(uint32_t s) {
-  // bits 6..15 of the presum, sign-extended from bit 15: (int16)s >> 6.
-  const int v = ((int)(s << 16)) >> 22;
-  return min(max(v, 0), 255);
-}
+// LDS by absolute byte address.  The kernel has no static LDS, so its dynamic
+// LDS (the StripeTables image) starts at address 0; addressing it through
+// integer-derived address-space-3 pointers lets every table address be one
+// VALU op (no symbol base to add).
+typedef __attribute__((address_space(3))) const uint8_t* lds_u8_ptr;
+typedef __attribute__((address_space(3))) const uint32_t* lds_u32_ptr;
+__device__ __forceinline__ uint32_t lds_u32(uint32_t addr) { return *(lds_u32_ptr)(uintptr_t)addr; }
+__device__ __forceinline__ uint32_t lds_u8(uint32_t addr) { return *(lds_u8_ptr)(uintptr_t)addr; }
 
-// YUYV word w (b0=Y0, b1=U, b2=Y1, b3=V) -> byte-spread detection masks of its
-// two pixels.  wc = w ^ 0xFF00FF00 (complemented chroma for the negative G
-// weights of WSEQ:188-190 on an unsigned dot product).
-// bank4 = 4 * (lane & 31): this lane's copy in the per-bank replicated tables
+// Phase 1 for both pixels of a YUYV word w (b0=Y0, b1=U, b2=Y1, b3=V):
+//  * presums of WSEQ:183-201 with v_dot4_u32_u8; wc =
+//    w ^ 0xFF00FF00 carries complemented chroma for the negative G weights
+//    (WSEQ:188-190);
+//  * x = (int16)presum >> 6 clamped to [0, 255] (WSEQ:203-205): the
+//    reference's _add2 keeps 16-bit lanes, so only bits 15:0 of the presum
+//    matter (B wraps for 27,136 triples) -- one v_bfe_i32 + one v_med3_i32;
+//  * max, min (WSEQ:207-216) and the hue case select of WSEQ:226-246
+//    (priority G > B > R on ties): diff and base;
+//  * LDS byte addresses of this pixel's LUT43[max - min] copy (per-bank
+//    replicated row, StripeTables::rows) and of its sat&val mask
+//    sv[max * 260 + min].
+// Plain 32-bit code: on gfx950 this kernel's time follows its VALU
+// instruction count (the 16-bit full-rate forms measured no faster in
+// context, scripts/ubench/pixel_mix.hip), and the compiler schedules it and
+// enforces the v_dot4 / VCC wait states itself.
+struct Phase1 { uint32_t m43_addr, sv_addr, diff, base; };
+__device__ __forceinline__ int clamp8_shift6(uint32_t s) {
+  const int x = ((int)(s << 16)) >> 22;  // bits 15:6, sign from 15 (v_bfe_i32)
+  const int lo = x < 0 ? 0 : x;
+  return lo > 255 ? 255 : lo;            // v_med3_i32
+}
 template <int PIX>
-__device__ __forceinline__ uint32_t detect(uint32_t w, uint32_t wc, const uint8_t* lds,
-                                           uint32_t m43_lane, uint32_t hue_lane) {
-  // presums of WSEQ:183-201
+__device__ __forceinline__ Phase1 phase1(uint32_t w, uint32_t wc, uint32_t m43_lane) {
   constexpr uint32_t kY = PIX == 0 ? 74u : (74u << 16);
-  const uint32_t sR = __builtin_amdgcn_udot4(w, kY | (102u << 24), (uint32_t)-14248, false);
-  const uint32_t sG = __builtin_amdgcn_udot4(wc, kY | (25u << 8) | (52u << 24), (uint32_t)-10939, false);
-  const uint32_t sB = __builtin_amdgcn_udot4(w, kY | (129u << 8), (uint32_t)-17672, false);
-  const int r = clamp8_shift6(sR), g = clamp8_shift6(sG), b = clamp8_shift6(sB);
-  // WSEQ:207-249: max/min, LUT43[delta], hue case G > B > R on ties
+  const int r = clamp8_shift6(__builtin_amdgcn_udot4(w, kY | (102u << 24), (uint32_t)-14248, false));
+  const int g = clamp8_shift6(__builtin_amdgcn_udot4(wc, kY | (25u << 8) | (52u << 24), (uint32_t)-10939, false));
+  const int b = clamp8_shift6(__builtin_amdgcn_udot4(w, kY | (129u << 8), (uint32_t)-17672, false));
   const int mx = max(r, max(g, b));
   const int mn = min(r, min(g, b));
-  const int m = (int)*reinterpret_cast<const uint32_t*>(lds + (((uint32_t)(mx - mn) << 7) + m43_lane));
-  const int dR = g - b, dG = b - r, dB = r - g;
+  Phase1 p;
+  p.m43_addr = ((uint32_t)(mx - mn) << 8) + m43_lane;
+  p.sv_addr = __umul24((uint32_t)mx, (uint32_t)kSvStride) + (uint32_t)mn;
   const bool eqG = mx == g, eqB = mx == b;
+  const int dR = g - b, dG = b - r, dB = r - g;
   int diff = eqB ? dB : dR;
-  diff = eqG ? dG : diff;
-  int base = eqB ? 43690 : 0;
-  base = eqG ? 21845 : base;
-  const uint32_t h = (uint32_t)(__mul24(m, diff) + base);  // m < 2^14, |diff| < 2^8
-  const uint32_t H = (h >> 8) & 0xFFu;
-  const uint32_t hue = *reinterpret_cast<const uint32_t*>(lds + ((H << 7) + hue_lane));
-  const uint32_t sv = lds[__mul24(mx, kSvStride) + mn];
-  // spread sv's bit t to bit 8t: terms at t + 7s are disjoint for t, s < 4
-  return hue & __mul24(sv, 0x00204081u);
+  p.diff = (uint32_t)(eqG ? dG : diff);
+  uint32_t base = eqB ? 43690u : 0u;
+  p.base = eqG ? 21845u : base;
+  return p;
+}
+
+// Phase 2: h = base + m * diff (WSEQ:226-246; m < 2^14, |diff| < 2^8, so one
+// v_mad_i32_i24), whose bits 15:8 (H) select the byte-spread hue mask (range t
+// -> bit 8t); returns the LDS byte address of this lane's copy.
+// (LLVM would fuse the multiply-add into a quarter-rate v_mad_u64_u32.)
+__device__ __forceinline__ uint32_t phase2_addr(uint32_t m, const Phase1& p, uint32_t hue_lane) {
+  uint32_t h;
+  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(h) : "v"(m), "v"(p.diff), "v"(p.base));
+  return (h & 0xFF00u) + hue_lane;
+}
+
+// Combine: spread sv's bit t to bit 8t (terms at t + 7s are disjoint for
+// t, s < 4) and AND with the hue mask.
+__device__ __forceinline__ uint32_t combine(uint32_t hue, uint32_t sv) {
+  return hue & __umul24(sv, 0x00204081u);
 }
 
 // Sum each of N values over the 64 lanes of the wave (result valid in lane
@@ -136,17 +169,18 @@ __device__ __forceinline__ uint32_t pack_bits(uint32_t e) {
 
 template <int LAYOUT, int NR, bool MASKS>
 __global__ __launch_bounds__(kMaxBlock) void stripe_kernel(KernelArgs a, StripeGeom g) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(a.stripe_tables);
-    uint4* dst = reinterpret_cast<uint4*>(lds);
+  {  // stage the tables at LDS address 0 (dynamic LDS, sizeof(StripeTables))
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4* src = reinterpret_cast<const u32x4*>(a.stripe_tables);
+    typedef __attribute__((address_space(3))) u32x4* lds_u128_wptr;
+    lds_u128_wptr dst = (lds_u128_wptr)(uintptr_t)0;
     for (int i = threadIdx.x; i < (int)(sizeof(StripeTables) / 16); i += blockDim.x) dst[i] = src[i];
   }
   __syncthreads();
 
   const int t = threadIdx.x;
-  const uint32_t m43_lane = (uint32_t)offsetof(StripeTables, m43) + ((t & 31) << 2);
-  const uint32_t hue_lane = (uint32_t)offsetof(StripeTables, hue) + ((t & 31) << 2);
+  const uint32_t hue_lane = (uint32_t)offsetof(StripeTables, rows) + kHueRowOffset + ((t & 31) << 2);
+  const uint32_t m43_lane = (uint32_t)offsetof(StripeTables, rows) + kM43RowOffset + ((t & 31) << 2);
   const bool active = t < g.k * g.cpr;
   const int col = active ? t % g.cpr : 0;
   const int ro = active ? t / g.cpr : 0;
@@ -194,13 +228,21 @@ __global__ __launch_bounds__(kMaxBlock) void stripe_kernel(KernelArgs a, StripeG
     // one step: 8 pixels of row y0 + s*k from the chunk words in `cw`
     auto step = [&](const uint32_t (&cw)[4], int s) {
       const bool valid = s < vsteps;
-      uint32_t e[8];
+      Phase1 p[8];
+      uint32_t m[8], sv[8], e[8];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t wc = cw[q] ^ 0xFF00FF00u;
-        e[2 * q] = detect<0>(cw[q], wc, lds, m43_lane, hue_lane);
-        e[2 * q + 1] = detect<1>(cw[q], wc, lds, m43_lane, hue_lane);
+        p[2 * q] = phase1<0>(cw[q], wc, m43_lane);
+        p[2 * q + 1] = phase1<1>(cw[q], wc, m43_lane);
       }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        m[j] = lds_u32(p[j].m43_addr);
+        sv[j] = lds_u8(p[j].sv_addr);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) e[j] = combine(lds_u32(phase2_addr(m[j], p[j], hue_lane)), sv[j]);
       if (MASKS && valid) {
         const int y = y0 + s * g.k;
         uint8_t* mp = a.masks + ((int64_t)f * a.height + y) * a.width + x0;

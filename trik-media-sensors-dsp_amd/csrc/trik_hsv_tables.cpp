@@ -76,8 +76,8 @@ void compile_stripe_tables(const RangeTables& base, int n, StripeTables* out) {
     uint32_t spread = 0;
     for (int t = 0; t < n && t < 4; ++t) spread |= ((uint32_t)(base.hue[i] >> t) & 1u) << (8 * t);
     for (int b = 0; b < kBanks; ++b) {
-      out->m43[i * kBanks + b] = base.lut43[i];
-      out->hue[i * kBanks + b] = spread;
+      out->rows[i][kHueRowOffset / 4 + b] = spread;
+      out->rows[i][kM43RowOffset / 4 + b] = base.lut43[i];
     }
   }
 }

@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libtrik_hsv.so")
+# TRIK_HSV_LIB overrides the library path (development A/B of kernel variants)
+LIB_PATH = os.environ.get("TRIK_HSV_LIB") or os.path.join(HERE, "libtrik_hsv.so")
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
 
 # return codes / commands / bits (TI ialg.h, xdm.h values)
