@@ -42,7 +42,8 @@ def parse():
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--targets", type=int, default=4)
     ap.add_argument("--kind", type=int, default=0, help="0 uniform random bytes, 1 scene")
-    ap.add_argument("--cpu-frames", type=int, default=1024, help="CPU baseline sample (frames)")
+    ap.add_argument("--cpu-frames", type=int, default=512, help="CPU baseline sample (frames)")
+    ap.add_argument("--cpu-frames-1core", type=int, default=32, help="single-thread CPU sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="rocprofv3 FETCH_SIZE summary used for roofline.traffic")
@@ -67,11 +68,29 @@ def cpu_baseline(args, width, height, ll, n_ranges, gpu_sums):
     sums, _ = oracle.batch(host, height * ll, n, width, height, ll, oracle.LAYOUT_YUYV,
                            RANGES[:n_ranges], n_threads=cores)
     dt = time.perf_counter() - t0
+    n1 = min(args.cpu_frames_1core, n)
+    t1 = time.perf_counter()
+    oracle.batch(host, height * ll, n1, width, height, ll, oracle.LAYOUT_YUYV, RANGES[:n_ranges],
+                 n_threads=1)
+    dt1 = time.perf_counter() - t1
     parity = bool(np.array_equal(sums, gpu_sums[:n]))
     return {"value": round(n * width * height / dt / 1e6, 3), "unit": "Mpix/s", "cores": cores,
             "kind": "port",
             "sample": f"{n} frames x {width}x{height} YUYV, {n_ranges} ranges "
-                      f"(frames 0..{n - 1} of the GPU batch), {cores} threads, {dt:.2f} s"}, parity
+                      f"(frames 0..{n - 1} of the GPU batch), {cores} threads, {dt:.2f} s",
+            "value_1core": round(n1 * width * height / dt1 / 1e6, 3),
+            "cpu_model": cpu_model()}, parity
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def load_traffic(path, bytes_per_launch):
@@ -91,6 +110,7 @@ def main():
     import torch.distributed as dist
 
     import trik_hsv
+    from trik_hsv.shard import all_reduce_totals, batch_totals, frame_shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -106,10 +126,11 @@ def main():
     ranges = RANGES[:T]
     frames = torch.empty(F * fb, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
-    trik_hsv.synth(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, args.kind, SEED, first_frame=rank * F)
+    first, count = frame_shard(world * F, rank, world)  # weak scaling: F frames per rank
+    assert count == F
+    trik_hsv.synth(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, args.kind, SEED, first_frame=first)
     det = trik_hsv.Detector()
     sums = torch.zeros((F, T, 3), dtype=torch.int64, device=dev)
-    totals = torch.zeros((T, 3), dtype=torch.int64, device=dev)
 
     def step(ev0=None, ev1=None):
         sums.zero_()
@@ -119,9 +140,7 @@ def main():
         if ev1 is not None:
             ev1.record(stream)
         targets = trik_hsv.batch_targets(sums, W, H, stream=stream)
-        torch.sum(sums, dim=0, out=totals)
-        if world > 1:
-            dist.all_reduce(totals)  # RCCL over xGMI: 3*T int64 per step
+        all_reduce_totals(batch_totals(sums))  # RCCL over xGMI when N > 1: 3*T int64 per step
         return targets
 
     for _ in range(args.warmup):
@@ -164,7 +183,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": load_traffic(args.pmc, bytes_per_launch),
-                     "kernel": "reduce_kernel<YUYV,4>", "kernel_ms": round(kern_ms, 4),
+                     "kernel": "stripe_kernel<YUYV,4>", "kernel_ms": round(kern_ms, 4),
                      "kernel_ms_max_rank": round(kern_ms_max, 4),
                      "bytes_per_launch": bytes_per_launch},
     }
