@@ -1,9 +1,12 @@
 // trik_hsv_kernels.hip -- CDNA4 (gfx950) kernels of the TRIK HSV path.
 //
-//  reduce_kernel   the hot path: one read-once pass over N frames of packed
-//                  YUYV (or ov7670 planes) that fuses WSEQ:251-284 (YUV->RGB->
-//                  HSV) with WSEQ:316-354 (threshold + per-row count / sumX /
-//                  sumY) for up to 4 ranges, and reduces per frame.
+//  reduce_kernel   the generic form of the hot path, used when the optimised
+//                  stripe_kernel (trik_hsv_stripe.hip) does not apply (input
+//                  not 16-byte aligned, width > 8192): one read-once pass
+//                  over N frames of packed YUYV (or ov7670 planes) fusing
+//                  WSEQ:251-284 (YUV->RGB->HSV) with WSEQ:316-354 (threshold +
+//                  per-row count / sumX / sumY) for up to 4 ranges, reduced
+//                  per frame.
 //  targets_kernel  WSEQ:486-505 epilogue in IEEE fp32, one thread per
 //                  (frame, range).
 //  synth_kernel    device-side synthetic frames (bit-identical to the CPU
