@@ -137,7 +137,7 @@ typedef struct TRIK_VIDTRANSCODE_CV_InArgsAlg {
   uint8_t detectSatTo;
   uint8_t detectValFrom;  /* [0..100] */
   uint8_t detectValTo;
-  int32_t autoDetectHsv;  /* not implemented: see INTEGRATION.md */
+  int32_t autoDetectHsv;  /* fill OutArgsAlg.detect* (WSEQ:455-462); detection unchanged */
 } TRIK_VIDTRANSCODE_CV_InArgsAlg;
 
 /* IVIDTRANSCODE_InArgs base fields used at WFXNS:192-224 */
@@ -242,9 +242,10 @@ int32_t TRIK_VIDTRANSCODE_CV_create(const TRIK_VIDTRANSCODE_CV_Params* params,
 int32_t TRIK_VIDTRANSCODE_CV_delete(TRIK_VIDTRANSCODE_CV_Handle handle);
 
 /* Replaces TRIK_VIDTRANSCODE_CV_process (WFXNS:174-264).  One host frame in
- * (in_bufs->descs[0]), targetX/Y/Size out in out_args->alg.  The preview
- * stream is zero-filled (WFXNS:234) but not rendered; numOutputStreams == 0
- * is accepted and writes nothing.  Returns IVIDTRANSCODE_EOK / _EFAIL /
+ * (in_bufs->descs[0]), targetX/Y/Size out in out_args->alg (and detect* when
+ * autoDetectHsv is set).  With numOutputStreams == 1 the RGB565X preview is
+ * rendered into out_bufs->bufs[0] (see trik_hsv_batch_preview);
+ * numOutputStreams == 0 is accepted and writes nothing.  Returns IVIDTRANSCODE_EOK / _EFAIL /
  * _EUNSUPPORTED with the reference's extendedError bits. */
 int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle handle,
                                      TRIK_XDM1_BufDesc* in_bufs, TRIK_XDM_BufDesc* out_bufs,
@@ -329,6 +330,28 @@ int32_t trik_hsv_batch_targets(const TrikHsvFrameBatch* batch, int32_t n_ranges,
 int32_t trik_hsv_batch_masks(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvFrameBatch* batch,
                              const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int32_t n_ranges,
                              uint8_t* masks_dev, TrikHsvTargetSums* sums_dev, void* hip_stream);
+
+/* The operator's preview stream for N frames and one range (SURVEY 8(f)
+ * row 2): each preview (out_height rows of out_line_length bytes at
+ * previews_dev + i * preview_stride) is zero-filled (WFXNS:234), then written
+ * as proceedImageHsv does -- RGB565X (B5 G6 R5, R in the low bits) of every
+ * source pixel through the truncated scale maps, last writer wins, detected
+ * pixels as 0x00ffff (WSEQ:316-354, 371-387) -- and overlaid with the guide
+ * lines and the target circle (WSEQ:66-166, 471-494).  The circle uses
+ * sums_dev[i * sums_pitch] (this range's sums of frame i, e.g. from
+ * trik_hsv_process_batch with sums_pitch = n_ranges). */
+int32_t trik_hsv_batch_preview(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvFrameBatch* batch,
+                               const TRIK_VIDTRANSCODE_CV_InArgsAlg* range,
+                               const TrikHsvTargetSums* sums_dev, int32_t sums_pitch,
+                               int32_t out_width, int32_t out_height, int32_t out_line_length,
+                               uint8_t* previews_dev, int64_t preview_stride, void* hip_stream);
+
+/* autoDetectHsv for N frames: HsvRangeDetector::detect
+ * (trik/webcam/object_sensor/include/internal/cv_hsv_range_detector.hpp:
+ * 88-198, zone scale 6 as WSEQ:32).  out_dev[i][6] = detectHue,
+ * detectHueTolerance, detectSat, detectSatTolerance, detectVal,
+ * detectValTolerance (uint16), as OutArgsAlg receives them. */
+int32_t trik_hsv_batch_auto_range(const TrikHsvFrameBatch* batch, uint16_t* out_dev, void* hip_stream);
 
 /* Fill batch->frames (device, writable) with synthetic frames; frame i of the
  * batch is global frame first_frame + i.  kind 0 = uniform random bytes,

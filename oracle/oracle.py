@@ -20,6 +20,14 @@ LAYOUT_YUYV = 0
 LAYOUT_OV7670 = 1
 
 
+class OutArgs(C.Structure):
+    _fields_ = [("target_x", C.c_int8), ("target_y", C.c_int8), ("target_size", C.c_uint8),
+                ("detect_written", C.c_uint8), ("detect_hue", C.c_uint16),
+                ("detect_hue_tol", C.c_uint16), ("detect_sat", C.c_uint16),
+                ("detect_sat_tol", C.c_uint16), ("detect_val", C.c_uint16),
+                ("detect_val_tol", C.c_uint16)]
+
+
 class Range(C.Structure):
     """Mirrors TRIK_VIDTRANSCODE_CV_InArgsAlg's HSV fields
     (trik/webcam/object_sensor/trik_vidtranscode_cv.h:48-56)."""
@@ -83,6 +91,10 @@ def lib():
         L.trik_oracle_synth.argtypes = [vp, i64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                         C.c_int, C.c_int, u64]
         L.trik_oracle_synth.restype = None
+        L.trik_oracle_run.argtypes = [vp, i64, C.c_int, C.c_int, C.c_int, C.c_int,
+                                      C.POINTER(Range), C.c_int, C.c_int, C.c_int, C.c_int, vp,
+                                      i64, C.POINTER(OutArgs)]
+        L.trik_oracle_run.restype = C.c_int
         _lib = L
     return _lib
 
@@ -173,3 +185,22 @@ def synth(n_frames, width, height, line_length, layout, kind, seed, first_frame=
     lib().trik_oracle_synth(_ptr(out), stride, first_frame, n_frames, width, height,
                             line_length, layout, kind, seed)
     return out
+
+
+def run(frame_u8: np.ndarray, width, height, line_length, layout, rng, auto_detect=False,
+        out_width=None, out_height=None, out_line_length=None, preview=True):
+    """BallDetector::setup + run for one frame and one range (WSEQ:358-508).
+
+    Returns (rc, outargs dict, preview uint8 array [out_height * out_line_length] or None)."""
+    fr = np.ascontiguousarray(frame_u8, dtype=np.uint8)
+    ow = width // 2 if out_width is None else out_width
+    oh = height // 2 if out_height is None else out_height
+    oll = 2 * ow if out_line_length is None else out_line_length
+    out = np.zeros(max(1, oh * oll), np.uint8) if preview else None
+    oa = OutArgs()
+    rc = lib().trik_oracle_run(_ptr(fr), fr.size, width, height, line_length, layout,
+                               C.byref(Range(*rng)), 1 if auto_detect else 0, ow, oh, oll,
+                               _ptr(out) if out is not None else None,
+                               out.size if out is not None else 0, C.byref(oa))
+    d = {k: getattr(oa, k) for k, _ in OutArgs._fields_}
+    return rc, d, (out[:oh * oll] if out is not None else None)

@@ -293,6 +293,22 @@ void trik_oracle_yuv_table(uint64_t* out, int closed) {
 
 #define TRIK_ORACLE_MAX_RANGES 64
 
+/* The YUYV word (Y0 U Y1 V) of pixels 2q, 2q+1 of a row: WSEQ:262-270 for
+ * packed YUYV; OSEQ:360-373 for the ov7670 planes (U = odd chroma byte,
+ * V = even chroma byte). */
+static uint32_t pair_word(const uint8_t* frame, int height, int line_length, int layout, int row,
+                          int q) {
+  if (layout == TRIK_ORACLE_LAYOUT_OV7670) {
+    const uint8_t* yrow = frame + (int64_t)row * line_length;
+    const uint8_t* crow = frame + (int64_t)line_length * height + (int64_t)row * line_length;
+    const uint32_t c = trik_c64x_swap4((uint32_t)crow[2 * q] | ((uint32_t)crow[2 * q + 1] << 8));
+    const uint32_t yy = (uint32_t)yrow[2 * q] | ((uint32_t)yrow[2 * q + 1] << 8);
+    return trik_c64x_unpklu4(yy) | (trik_c64x_unpklu4(c) << 8);
+  }
+  const uint8_t* p = frame + (int64_t)row * line_length + 4 * q;
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
 int trik_oracle_frame(const uint8_t* frame, int64_t frame_size, int width, int height,
                       int line_length, int layout, const trik_oracle_range* ranges,
                       int n_ranges, int64_t* sums, uint8_t* mask) {
@@ -315,18 +331,7 @@ int trik_oracle_frame(const uint8_t* frame, int64_t frame_size, int width, int h
     uint32_t row_n[TRIK_ORACLE_MAX_RANGES], row_x[TRIK_ORACLE_MAX_RANGES];
     for (int t = 0; t < n_ranges; ++t) { row_n[t] = 0; row_x[t] = 0; }
     for (int q = 0; q < width / 2; ++q) { /* one YUYV word = pixels 2q, 2q+1 */
-      uint32_t yuyv;
-      if (layout == TRIK_ORACLE_LAYOUT_OV7670) {
-        /* OSEQ:369-373: U = odd chroma byte, V = even chroma byte */
-        const uint8_t* yrow = frame + (int64_t)row * line_length;
-        const uint8_t* crow = frame + (int64_t)line_length * height + (int64_t)row * line_length;
-        const uint32_t c = trik_c64x_swap4((uint32_t)crow[2 * q] | ((uint32_t)crow[2 * q + 1] << 8));
-        const uint32_t yy = (uint32_t)yrow[2 * q] | ((uint32_t)yrow[2 * q + 1] << 8);
-        yuyv = trik_c64x_unpklu4(yy) | (trik_c64x_unpklu4(c) << 8);
-      } else {
-        const uint8_t* p = frame + (int64_t)row * line_length + 4 * q;
-        yuyv = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-      }
+      const uint32_t yuyv = pair_word(frame, height, line_length, layout, row, q);
       uint32_t rgb[2];
       trik_oracle_pair_rgb_c64x(yuyv, rgb);
       for (int k = 0; k < 2; ++k) {
@@ -499,4 +504,195 @@ void trik_oracle_synth(uint8_t* frames, int64_t frame_stride, int first_frame, i
         }
       }
   }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Whole run: preview, overlays, auto HSV range (WSEQ:358-508).              */
+/* ------------------------------------------------------------------------ */
+
+static int32_t clamp_i32(int32_t lo, int32_t v, int32_t hi) { /* range<T>, stdcpp.hpp:38-44 */
+  if (v < lo) return lo;
+  if (v > hi) return hi;
+  return v;
+}
+
+typedef struct run_ctx {
+  int width, height, out_line_length;
+  const uint32_t* wi2wo;
+  const uint32_t* hi2ho;
+  uint8_t* out;
+} run_ctx;
+
+/* writeOutputPixel, WSEQ:66-70: 0x00RRGGBB -> B5 G6 R5 with R in the low bits */
+static void write_px(uint8_t* dst, uint32_t rgb888) {
+  const uint16_t v = (uint16_t)(((rgb888 >> 19) & 0x001f) | ((rgb888 >> 5) & 0x07e0) |
+                                ((rgb888 << 8) & 0xf800));
+  dst[0] = (uint8_t)v;
+  dst[1] = (uint8_t)(v >> 8);
+}
+
+/* drawOutputPixelBound, WSEQ:72-89 (the source point is clamped to the image) */
+static void draw_bound(const run_ctx* c, int32_t col, int32_t row, uint32_t rgb888) {
+  const int32_t sc = clamp_i32(0, col, c->width - 1);
+  const int32_t sr = clamp_i32(0, row, c->height - 1);
+  const int64_t ofs = (int64_t)(int32_t)c->hi2ho[sr] * c->out_line_length +
+                      (int64_t)(int32_t)c->wi2wo[sc] * 2;
+  write_px(c->out + ofs, rgb888);
+}
+
+/* drawOutputCircle, WSEQ:91-134 (midpoint circle) */
+static void draw_circle(const run_ctx* c, int32_t col, int32_t row, int32_t radius, uint32_t rgb) {
+  int32_t err = 1 - radius, err_y = 1, err_x = -2 * radius, x = radius, y = 0;
+  draw_bound(c, col, row + radius, rgb);
+  draw_bound(c, col, row - radius, rgb);
+  draw_bound(c, col + radius, row, rgb);
+  draw_bound(c, col - radius, row, rgb);
+  while (y < x) {
+    if (err >= 0) {
+      x -= 1;
+      err_x += 2;
+      err += err_x;
+    }
+    y += 1;
+    err_y += 2;
+    err += err_y;
+    draw_bound(c, col + x, row + y, rgb);
+    draw_bound(c, col + x, row - y, rgb);
+    draw_bound(c, col - x, row + y, rgb);
+    draw_bound(c, col - x, row - y, rgb);
+    draw_bound(c, col + y, row + x, rgb);
+    draw_bound(c, col + y, row - x, rgb);
+    draw_bound(c, col - y, row + x, rgb);
+    draw_bound(c, col - y, row - x, rgb);
+  }
+}
+
+/* drawRgbTargetCenterLine / ...HorizontalCenterLine, WSEQ:136-166 */
+static void draw_vline(const run_ctx* c, int32_t col, int32_t row, uint32_t rgb) {
+  for (int adj = 0; adj < 100; ++adj) {
+    draw_bound(c, col, row - adj, rgb);
+    draw_bound(c, col, row + adj, rgb);
+  }
+}
+static void draw_hline(const run_ctx* c, int32_t col, int32_t row, uint32_t rgb) {
+  for (int adj = 0; adj < 100; ++adj) {
+    draw_bound(c, col - adj, row, rgb);
+    draw_bound(c, col + adj, row, rgb);
+  }
+}
+
+/* HsvRangeDetector (cv_hsv_range_detector.hpp:79-198): H/S/V histograms of
+ * the central zone; the value whose count first exceeds the running maximum
+ * (scan order, strict >) wins; scaled by float constants in double. */
+static void auto_range(const uint64_t* img, int width, int height, int zone_scale,
+                       trik_oracle_outargs* oa) {
+  const uint16_t h_height = (uint16_t)(height / 2), h_width = (uint16_t)(width / 2);
+  const uint16_t step = (uint16_t)(height / zone_scale);
+  const uint16_t left_p = (uint16_t)(h_width - step), right_p = (uint16_t)(h_width + step);
+  const uint16_t top_p = (uint16_t)(h_height - step), bot_p = (uint16_t)(h_height + step);
+  uint32_t hh[256], hs[256], hv[256];
+  memset(hh, 0, sizeof hh);
+  memset(hs, 0, sizeof hs);
+  memset(hv, 0, sizeof hv);
+  uint32_t max_h = 0, max_s = 0, max_v = 0;
+  int32_t max_hc = 0, max_sc = 0, max_vc = 0;
+  for (int row = 0; row < height; ++row)
+    for (int col = 0; col < width; ++col) {
+      const uint32_t p = (uint32_t)img[(int64_t)row * width + col];
+      const uint8_t h = (uint8_t)p, s = (uint8_t)(p >> 8), v = (uint8_t)(p >> 16);
+      if (left_p < col && right_p > col && top_p < row && bot_p > row) {
+        hh[h]++;
+        hs[s]++;
+        hv[v]++;
+        if (hh[h] > (uint32_t)max_hc) { max_h = h; max_hc = (int32_t)hh[h]; }
+        if (hs[s] > (uint32_t)max_sc) { max_s = s; max_sc = (int32_t)hs[s]; }
+        if (hv[v] > (uint32_t)max_vc) { max_v = v; max_vc = (int32_t)hv[v]; }
+      }
+    }
+  oa->detect_hue = (uint16_t)((double)max_h * 1.4f);
+  oa->detect_hue_tol = 15;
+  oa->detect_sat = (uint16_t)((double)max_s * 0.39f);
+  oa->detect_sat_tol = 30;
+  oa->detect_val = (uint16_t)((double)max_v * 0.39f);
+  oa->detect_val_tol = 30;
+  oa->detect_written = 1;
+}
+
+int trik_oracle_run(const uint8_t* frame, int64_t frame_size, int width, int height,
+                    int line_length, int layout, const trik_oracle_range* range, int auto_detect,
+                    int out_width, int out_height, int out_line_length, uint8_t* out,
+                    int64_t out_size, trik_oracle_outargs* oa) {
+  enum { kZoneScale = 6 }; /* WSEQ:32 */
+  memset(oa, 0, sizeof *oa);
+  if (width < 0 || height < 0 || width % 32 != 0 || height % 4 != 0) return -1; /* WSEQ:365-369 */
+  const int64_t need = (int64_t)height * line_length * (layout == TRIK_ORACLE_LAYOUT_OV7670 ? 2 : 1);
+  if ((int64_t)height * line_length > frame_size || need > frame_size) return -1; /* WSEQ:415 */
+  if (out && (int64_t)out_height * out_line_length > out_size) return -1;          /* WSEQ:417 */
+
+  /* WSEQ:371-387: scale maps, truncated double products */
+  const double sw = (double)out_width / width, sh = (double)out_height / height;
+  const double shift = sw < sh ? sw : sh;
+  uint32_t* wi2wo = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(width > 0 ? width : 1));
+  uint32_t* hi2ho = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(height > 0 ? height : 1));
+  uint64_t* img = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)((int64_t)width * height > 0 ? (int64_t)width * height : 1));
+  if (!wi2wo || !hi2ho || !img) {
+    free(wi2wo); free(hi2ho); free(img);
+    return -1;
+  }
+  for (int i = 0; i < width; ++i) wi2wo[i] = (uint32_t)(i * shift);
+  for (int i = 0; i < height; ++i) hi2ho[i] = (uint32_t)(i * shift);
+
+  uint32_t from, to, expect;
+  trik_oracle_pack_range(range, &from, &to, &expect);
+  int32_t tx = 0, ty = 0;
+  uint32_t tn = 0;
+  const run_ctx ctx = {width, height, out_line_length, wi2wo, hi2ho, out};
+  if (height > 0 && width > 0) {
+    for (int row = 0; row < height; ++row) /* convertImageYuyvToHsv */
+      for (int q = 0; q < width / 2; ++q) {
+        uint32_t rgb[2];
+        trik_oracle_pair_rgb_c64x(pair_word(frame, height, line_length, layout, row, q), rgb);
+        for (int k = 0; k < 2; ++k)
+          img[(int64_t)row * width + 2 * q + k] =
+              ((uint64_t)rgb[k] << 32) | trik_oracle_hsv_c64x(rgb[k]);
+      }
+    if (auto_detect) auto_range(img, width, height, kZoneScale, oa);
+    for (int row = 0; row < height; ++row) { /* proceedImageHsv */
+      uint32_t row_n = 0, row_x = 0;
+      for (int col = 0; col < width; ++col) {
+        const uint64_t e = img[(int64_t)row * width + col];
+        const int det = trik_oracle_detect((uint32_t)e, from, to, expect);
+        row_n += (uint32_t)det;
+        row_x += det ? (uint32_t)col : 0;
+        if (out)
+          write_px(out + (int64_t)hi2ho[row] * out_line_length + (int64_t)wi2wo[col] * 2,
+                   det ? 0x00ffffu : (uint32_t)(e >> 32));
+      }
+      tx += (int32_t)row_x;
+      ty += (int32_t)((uint32_t)row * row_n);
+      tn += row_n;
+    }
+  }
+  if (out && width > 0 && height > 0) { /* WSEQ:471-485 (degenerate sizes would index s_hi2ho[-1]) */
+    const int step = height / kZoneScale, h_height = height / 2, h_width = width / 2;
+    draw_vline(&ctx, h_width - 2 * step, h_height, 0xff00ff);
+    draw_vline(&ctx, h_width - step, h_height, 0xff00ff);
+    draw_vline(&ctx, h_width + step, h_height, 0xff00ff);
+    draw_vline(&ctx, h_width + 2 * step, h_height, 0xff00ff);
+    draw_hline(&ctx, h_width, h_height - 2 * step, 0xff00ff);
+    draw_hline(&ctx, h_width, h_height - step, 0xff00ff);
+    draw_hline(&ctx, h_width, h_height + step, 0xff00ff);
+    draw_hline(&ctx, h_width, h_height + 2 * step, 0xff00ff);
+  }
+  const int64_t sums[3] = {(int64_t)tn, (int64_t)tx, (int64_t)ty};
+  trik_oracle_targets(sums, width, height, &oa->target_x, &oa->target_y, &oa->target_size);
+  if (out && tn > 0) { /* WSEQ:486-494 */
+    const int32_t cx = (int32_t)((uint32_t)tx / tn), cy = (int32_t)((uint32_t)ty / tn);
+    const uint32_t radius = (uint32_t)ceilf(sqrtf((float)tn / 3.1415927f));
+    draw_circle(&ctx, cx, cy, (int32_t)radius, 0xffff00);
+  }
+  free(wi2wo);
+  free(hi2ho);
+  free(img);
+  return 0;
 }

@@ -114,11 +114,36 @@ int      trik_oracle_batch(const uint8_t* frames, int64_t frame_stride, int n_fr
                            int64_t* sums, int8_t* targets, int n_threads);
 
 /* Synthetic frame generators shared bit-for-bit with the device generator
- * (trik-media-sensors-dsp_amd/csrc/trik_hsv_synth.hip).
+ * (synth kernels in trik-media-sensors-dsp_amd/csrc/trik_hsv_kernels.hip).
  * kind 0 = uniform random bytes, kind 1 = scene (gradients + 6 discs). */
 void     trik_oracle_synth(uint8_t* frames, int64_t frame_stride, int first_frame,
                            int n_frames, int width, int height, int line_length,
                            int layout, int kind, uint64_t seed);
+
+/* OutArgsAlg fields written by one run (WPUB:64-74). */
+typedef struct trik_oracle_outargs {
+  int8_t target_x, target_y;
+  uint8_t target_size;
+  uint8_t detect_written; /* 1 when autoDetectHsv filled the detect* fields */
+  uint16_t detect_hue, detect_hue_tol, detect_sat, detect_sat_tol, detect_val, detect_val_tol;
+} trik_oracle_outargs;
+
+/* The whole of BallDetector::setup + run (WSEQ:358-508) for one frame and one
+ * range, as the codec's process() drives it:
+ *   - per-pixel RGB/HSV image (WSEQ:251-284, or the OSEQ:343-387 layout);
+ *   - autoDetectHsv: HsvRangeDetector::detect (cv_hsv_range_detector.hpp:
+ *     88-201, zone scale 6, WSEQ:32,455-462) into the detect* fields;
+ *   - proceedImageHsv (WSEQ:316-354): sums, and the RGB565X preview written
+ *     through the truncated double scale maps (WSEQ:371-387), detected pixels
+ *     as 0x00ffff, last writer wins;
+ *   - guide lines and target circle (WSEQ:66-166, 471-485), then OutArgs
+ *     (WSEQ:486-505).
+ * out may be NULL (no preview stream).  Returns 0, or -1 where setup/run
+ * would fail (geometry WSEQ:365-369, buffer sizes WSEQ:415-418). */
+int      trik_oracle_run(const uint8_t* frame, int64_t frame_size, int width, int height,
+                         int line_length, int layout, const trik_oracle_range* range,
+                         int auto_detect, int out_width, int out_height, int out_line_length,
+                         uint8_t* out, int64_t out_size, trik_oracle_outargs* oa);
 
 #ifdef __cplusplus
 }

@@ -1,3 +1,4 @@
+import json
 import os
 import sys
 
@@ -19,3 +20,15 @@ def oracle_mod():
 
     oracle.build()
     return oracle
+
+
+@pytest.fixture(scope="session")
+def golden():
+    with open(os.path.join(ROOT, "tests", "golden", "oracle_golden.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def table(oracle_mod):
+    """The oracle's 2^24-entry (rgb << 32 | hsv) table, index Y | U<<8 | V<<16."""
+    return oracle_mod.yuv_table(closed=False)

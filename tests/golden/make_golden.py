@@ -55,6 +55,19 @@ CASES = [
 ]
 
 
+# Whole BallDetector::run cases (trik_oracle_run): preview stream + OutArgs,
+# with and without autoDetectHsv.  name, W, H, lineLength, layout, kind, seed,
+# frame, range, auto, outW, outH, outLineLength
+RUN_CASES = [
+    ("run_640x480_scene_T0_auto", 640, 480, 1280, O.LAYOUT_YUYV, 1, 0x7A1C, 2, "T0", 1, 320, 240, 640),
+    ("run_640x480_uniform_T3_auto", 640, 480, 1280, O.LAYOUT_YUYV, 0, 0x7A1C, 5, "T3_wrap", 1, 320, 240, 640),
+    ("run_320x240_scene_full_scale0.625", 320, 240, 640, O.LAYOUT_YUYV, 1, 7, 0, "full", 0, 200, 150, 401),
+    ("run_ov7670_320x240_scene_T1", 320, 240, 320, O.LAYOUT_OV7670, 1, 7, 4, "T1", 1, 160, 120, 320),
+    ("run_32x480_zone_wrap", 32, 480, 64, O.LAYOUT_YUYV, 1, 3, 0, "T0", 1, 16, 240, 32),
+    ("run_empty_point_no_circle", 320, 240, 640, O.LAYOUT_YUYV, 1, 3, 1, "empty_point", 1, 160, 120, 320),
+]
+
+
 def main():
     out = {"generator": "tests/golden/make_golden.py", "ranges": RANGES}
     a = O.yuv_table(closed=False)
@@ -80,6 +93,19 @@ def main():
             "sums": sums.tolist(), "targets": tg,
         })
     out["cases"] = cases
+    runs = []
+    for name, w, h, ll, layout, kind, seed, fidx, rname, auto, ow, oh, oll in RUN_CASES:
+        fr = O.synth(1, w, h, ll, layout, kind, seed, first_frame=fidx)
+        rc, oa, pv = O.run(fr, w, h, ll, layout, RANGES[rname], auto_detect=bool(auto),
+                           out_width=ow, out_height=oh, out_line_length=oll)
+        assert rc == 0, name
+        runs.append({
+            "name": name, "width": w, "height": h, "line_length": ll, "layout": layout,
+            "kind": kind, "seed": seed, "frame": fidx, "range": rname, "auto": auto,
+            "out_width": ow, "out_height": oh, "out_line_length": oll,
+            "preview_sha256": hashlib.sha256(pv.tobytes()).hexdigest(), "outargs": oa,
+        })
+    out["runs"] = runs
     with open(os.path.join(HERE, "oracle_golden.json"), "w") as f:
         json.dump(out, f, indent=1)
     print("wrote", len(cases), "cases")

@@ -46,7 +46,7 @@ def test_process_matches_oracle(hsv, oracle_mod, kind, rng):
     s = hsv.ObjectSensor()
     assert s.set_params(w, h, ll) == 0
     frame = oracle_mod.synth(1, w, h, ll, LAYOUT_YUYV, kind, 0x7A1C, first_frame=9)
-    out = np.full(240 * 640, 0xAB, np.uint8)
+    out = np.full(240 * 640 + 64, 0xAB, np.uint8)
     rc, oa = s.process(frame, rng, out_buffer=out)
     assert rc == 0
     want = oracle_mod.targets(oracle_mod.frame(frame, w, h, ll, LAYOUT_YUYV, [rng])[0][0], w, h)
@@ -54,7 +54,9 @@ def test_process_matches_oracle(hsv, oracle_mod, kind, rng):
     assert oa.base.encodedBuf[0].bufSize == 240 * 640          # WSEQ:419
     assert oa.base.bitsConsumed == frame.size * 8
     assert oa.base.outputID[0] == 0 and oa.base.outBufsInUseFlag == 0
-    assert not out.any()                                        # zero-filled (WFXNS:234)
+    _, _, preview = oracle_mod.run(frame, w, h, ll, LAYOUT_YUYV, rng)
+    assert np.array_equal(out[:240 * 640], preview)            # rendered preview (WSEQ:316-354)
+    assert not out[240 * 640:].any()                            # rest zero-filled (WFXNS:234)
     s.close()
 
 

@@ -2,24 +2,9 @@
 pinned by: TI intrinsic semantics, the two independent derivations, the SURVEY
 Appendix A known-answer table and the committed golden fixtures."""
 import hashlib
-import json
-import os
 
 import numpy as np
 import pytest
-
-GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "oracle_golden.json")
-
-
-@pytest.fixture(scope="module")
-def golden():
-    with open(GOLDEN) as f:
-        return json.load(f)
-
-
-@pytest.fixture(scope="module")
-def table(oracle_mod):
-    return oracle_mod.yuv_table(closed=False)
 
 
 # --- per-intrinsic unit tests (hand-derived from TI's documented C64x+ semantics) ---

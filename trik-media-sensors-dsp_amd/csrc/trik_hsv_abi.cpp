@@ -112,8 +112,17 @@ struct TrikCvHandle {
   StripeTables* h_stripe = nullptr;
   hipEvent_t tables_busy = nullptr;
 
+  // preview geometry: scale maps for maps_key = {W, H, out_w, out_h}
+  uint32_t* d_maps = nullptr;
+  size_t d_maps_cap = 0;
+  int maps_key[4] = {-1, -1, -1, -1};
+  std::vector<uint32_t> h_maps;
+
   // process() staging
   hipStream_t stream = nullptr;
+  uint8_t* d_preview = nullptr;
+  size_t d_preview_cap = 0;
+  uint16_t* d_auto = nullptr;
   uint8_t* d_frame = nullptr;
   size_t d_frame_cap = 0;
   TrikHsvTargetSums* d_sums = nullptr;
@@ -134,6 +143,9 @@ void release(TrikCvHandle* h) {
   (void)hipFree(h->d_stripe);
   (void)hipHostFree(h->h_stripe);
   (void)hipFree(h->d_frame);
+  (void)hipFree(h->d_maps);
+  (void)hipFree(h->d_preview);
+  (void)hipFree(h->d_auto);
   (void)hipFree(h->d_sums);
   (void)hipFree(h->d_targets);
   if (h->tables_busy) (void)hipEventDestroy(h->tables_busy);
@@ -267,6 +279,56 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
 }
 
 inline void set_bit(int32_t& word, int bit) { word |= (int32_t)(1u << bit); }
+
+// Scale maps of the preview (WSEQ:371-387) for this geometry, uploaded once.
+int32_t ensure_maps(TrikCvHandle* h, int w, int hgt, int ow, int oh, hipStream_t s) {
+  if (h->d_maps && h->maps_key[0] == w && h->maps_key[1] == hgt && h->maps_key[2] == ow &&
+      h->maps_key[3] == oh)
+    return 0;
+  const size_t n = (size_t)w + hgt + ow + oh;
+  if (h->tables_busy) HIP_TRY(hipEventSynchronize(h->tables_busy));  // previous users done
+  if (n > h->d_maps_cap) {
+    (void)hipFree(h->d_maps);
+    h->d_maps = nullptr; h->d_maps_cap = 0;
+    HIP_TRY(hipMalloc(&h->d_maps, sizeof(uint32_t) * (n ? n : 1)));
+    h->d_maps_cap = n;
+  }
+  h->h_maps.assign(n ? n : 1, 0u);
+  preview_maps(w, hgt, ow, oh, h->h_maps.data());
+  HIP_TRY(hipMemcpyAsync(h->d_maps, h->h_maps.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipStreamSynchronize(s));  // h_maps is pageable and reused
+  h->maps_key[0] = w; h->maps_key[1] = hgt; h->maps_key[2] = ow; h->maps_key[3] = oh;
+  return 0;
+}
+
+PreviewArgs preview_args(const TrikCvHandle* h, const TrikHsvFrameBatch& b, int ow, int oh, int oll,
+                         uint8_t* previews, int64_t stride) {
+  PreviewArgs a;
+  a.frames = static_cast<const uint8_t*>(b.frames);
+  a.frame_stride = b.frame_stride;
+  a.n_frames = b.n_frames;
+  a.width = b.width; a.height = b.height; a.line_length = b.line_length; a.layout = b.layout;
+  a.tables = h->d_tables;
+  a.out_w = ow; a.out_h = oh; a.out_ll = oll;
+  a.previews = previews;
+  a.preview_stride = stride;
+  a.wi2wo = h->d_maps;
+  a.hi2ho = a.wi2wo + b.width;
+  a.last_row = reinterpret_cast<const int32_t*>(a.hi2ho + b.height);
+  a.last_col = a.last_row + oh;
+  return a;
+}
+
+AutoRangeArgs auto_range_args(const TrikHsvFrameBatch& b, uint16_t* out) {
+  AutoRangeArgs a;
+  a.frames = static_cast<const uint8_t*>(b.frames);
+  a.frame_stride = b.frame_stride;
+  a.n_frames = b.n_frames;
+  a.width = b.width; a.height = b.height; a.line_length = b.line_length; a.layout = b.layout;
+  auto_range_zone(b.width, b.height, a.c_lo, a.c_hi, a.r_lo, a.r_hi);
+  a.out = out;
+  return a;
+}
 
 }  // namespace
 
@@ -424,18 +486,45 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
         int32_t r = run_sums(h, &b, &in_args->alg, 1, h->d_sums, nullptr, h->stream);
         if (r) return r;
         HIP_TRY(launch_targets(b, 1, h->d_sums, h->d_targets, h->stream));
+        uint16_t detect[6] = {0, 0, 0, 0, 0, 0};
+        const bool auto_detect = in_args->alg.autoDetectHsv != 0;
+        if (auto_detect) {  // WSEQ:455-462
+          if (!h->d_auto) HIP_TRY(hipMalloc(&h->d_auto, 6 * sizeof(uint16_t)));
+          HIP_TRY(launch_auto_range(auto_range_args(b, h->d_auto), h->stream));
+          HIP_TRY(hipMemcpyAsync(detect, h->d_auto, sizeof detect, hipMemcpyDeviceToHost, h->stream));
+        }
+        if (out_ptr && out_size > 0) {  // the preview stream (WSEQ:316-354, 471-494)
+          const size_t pb = (size_t)out_size;
+          if (pb > h->d_preview_cap) {
+            (void)hipFree(h->d_preview);
+            h->d_preview = nullptr; h->d_preview_cap = 0;
+            HIP_TRY(hipMalloc(&h->d_preview, pb));
+            h->d_preview_cap = pb;
+          }
+          r = ensure_maps(h, h->in_w, h->in_h, h->out_w, h->out_h, h->stream);
+          if (r) return r;
+          HIP_TRY(hipMemsetAsync(h->d_preview, 0, pb, h->stream));
+          const PreviewArgs pa = preview_args(h, b, h->out_w, h->out_h, h->out_ll, h->d_preview,
+                                              (int64_t)pb);
+          HIP_TRY(launch_preview(pa, h->d_sums, 1, h->stream));
+          HIP_TRY(hipMemcpyAsync(out_ptr, h->d_preview, pb, hipMemcpyDeviceToHost, h->stream));
+        }
         TrikHsvTarget t;
         HIP_TRY(hipMemcpyAsync(&t, h->d_targets, sizeof t, hipMemcpyDeviceToHost, h->stream));
         HIP_TRY(hipStreamSynchronize(h->stream));
         oa.targetX = t.x; oa.targetY = t.y; oa.targetSize = t.size;
+        if (auto_detect) {
+          oa.detectHue = detect[0]; oa.detectHueTolerance = detect[1];
+          oa.detectSat = detect[2]; oa.detectSatTolerance = detect[3];
+          oa.detectVal = detect[4]; oa.detectValTolerance = detect[5];
+        }
         return 0;
       };
       const int32_t r = body();
       if (switched) (void)hipSetDevice(prev);
       if (r) { rc = TRIK_IVIDTRANSCODE_EFAIL; why = g_last_error; }
     }
-    // autoDetectHsv (WSEQ:455-462) is not implemented: OutArgs.detect* are
-    // left untouched, as the reference does when the flag is clear.
+    // OutArgs.detect* are written only when autoDetectHsv is set (WSEQ:455-462)
   }
   if (rc != TRIK_IVIDTRANSCODE_EOK) {
     set_bit(out_args->base.extendedError, TRIK_XDM_CORRUPTEDDATA_BIT);  // WFXNS:243-247
@@ -520,6 +609,45 @@ extern "C" int32_t trik_hsv_batch_masks(TRIK_VIDTRANSCODE_CV_Handle h, const Tri
   if (!masks && b->n_frames > 0) return fail(TRIK_IVIDTRANSCODE_EFAIL, "masks is NULL");
   std::lock_guard<std::mutex> lock(h->mu);
   return run_sums(h, b, ranges, n, sums, masks, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int32_t trik_hsv_batch_preview(TRIK_VIDTRANSCODE_CV_Handle h, const TrikHsvFrameBatch* b,
+                                          const TRIK_VIDTRANSCODE_CV_InArgsAlg* range,
+                                          const TrikHsvTargetSums* sums, int32_t sums_pitch,
+                                          int32_t out_width, int32_t out_height,
+                                          int32_t out_line_length, uint8_t* previews,
+                                          int64_t preview_stride, void* stream) {
+  int32_t rc = check_common(h, b, range, 1, sums);
+  if (rc) return rc;
+  if (out_width < 0 || out_height < 0 || out_line_length < 2 * out_width || sums_pitch < 1)
+    return fail(TRIK_IVIDTRANSCODE_EFAIL, "preview geometry: need out_line_length >= 2*out_width, sums_pitch >= 1");
+  const int64_t pb = (int64_t)out_height * out_line_length;
+  if (b->n_frames > 1 && preview_stride < pb)
+    return fail(TRIK_IVIDTRANSCODE_EFAIL, "preview_stride smaller than one preview");
+  if (!previews && b->n_frames > 0 && pb > 0) return fail(TRIK_IVIDTRANSCODE_EFAIL, "previews is NULL");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  std::lock_guard<std::mutex> lock(h->mu);
+  if (b->n_frames == 0 || pb == 0) return 0;
+  HIP_TRY(hipMemset2DAsync(previews, (size_t)(b->n_frames > 1 ? preview_stride : pb), 0, (size_t)pb,
+                           (size_t)b->n_frames, s));  // WFXNS:234 zero fill
+  if (b->width == 0 || b->height == 0) return 0;
+  rc = ensure_tables(h, range, 1, s);
+  if (rc) return rc;
+  rc = ensure_maps(h, b->width, b->height, out_width, out_height, s);
+  if (rc) return rc;
+  HIP_TRY(launch_preview(preview_args(h, *b, out_width, out_height, out_line_length, previews,
+                                      preview_stride), sums, sums_pitch, s));
+  if (!h->tables_busy) HIP_TRY(hipEventCreateWithFlags(&h->tables_busy, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(h->tables_busy, s));
+  return 0;
+}
+
+extern "C" int32_t trik_hsv_batch_auto_range(const TrikHsvFrameBatch* b, uint16_t* out, void* stream) {
+  const std::string e = validate_batch(b);
+  if (!e.empty()) return fail(TRIK_IVIDTRANSCODE_EFAIL, e);
+  if (!out && b->n_frames > 0) return fail(TRIK_IVIDTRANSCODE_EFAIL, "out is NULL");
+  HIP_TRY(launch_auto_range(auto_range_args(*b, out), static_cast<hipStream_t>(stream)));
+  return 0;
 }
 
 extern "C" int32_t trik_hsv_synth(const TrikHsvFrameBatch* b, int32_t first_frame, int32_t kind,

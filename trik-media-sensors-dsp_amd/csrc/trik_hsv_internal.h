@@ -19,13 +19,14 @@ constexpr int kRangesPerLaunch = 4;
 //                       pixel with max channel mx and min channel mn (mn <= mx).
 //                       S = (LUT255[mx] * (mx - mn)) >> 8 (WSEQ:223-224), V = mx.
 //   hue[H]            : bit t = range t's hue test passes (incl. wrap, WSEQ:433-445).
-//   lut43[d]          : s_mult43_div (WSEQ:389-407).
+//   lut43[d], lut255[m] : s_mult43_div, s_mult255_div (WSEQ:389-407).
 struct alignas(16) RangeTables {
   uint8_t sv[256 * 256];
   uint8_t hue[256];
   uint16_t lut43[256];
+  uint16_t lut255[256];
 };
-static_assert(sizeof(RangeTables) == 65536 + 256 + 512, "table layout");
+static_assert(sizeof(RangeTables) == 65536 + 256 + 512 + 512, "table layout");
 
 // Packed form of one InArgs range (WSEQ:425-445).
 struct PackedRange {
@@ -73,7 +74,32 @@ struct KernelArgs {
   int32_t mask_shift;    // bit position of this launch's range 0 in the mask byte
 };
 
-// Launchers (trik_hsv_kernels.hip).  Return hipError_t as int.
+// RGB565X preview of N frames for one range (trik_hsv_operator.hip).
+struct PreviewArgs {
+  const uint8_t* frames;
+  int64_t frame_stride;
+  int32_t n_frames, width, height, line_length, layout;
+  const RangeTables* tables;  // range 0 of these tables is the preview's range
+  int32_t out_w, out_h, out_ll;
+  uint8_t* previews;
+  int64_t preview_stride;
+  const int32_t* last_row;  // [out_h]: last source row mapped to each output row, or -1
+  const int32_t* last_col;  // [out_w]
+  const uint32_t* wi2wo;    // [width]  WSEQ:375-379
+  const uint32_t* hi2ho;    // [height] WSEQ:381-385
+};
+
+// Auto HSV range of N frames (trik_hsv_operator.hip); out[f][6] = detectHue,
+// detectHueTolerance, detectSat, detectSatTolerance, detectVal, detectValTolerance.
+struct AutoRangeArgs {
+  const uint8_t* frames;
+  int64_t frame_stride;
+  int32_t n_frames, width, height, line_length, layout;
+  int32_t c_lo, c_hi, r_lo, r_hi;  // exclusive zone bounds (uint16 values, hpp:88-108)
+  uint16_t* out;
+};
+
+// Launchers (trik_hsv_kernels.hip, trik_hsv_operator.hip).  Return hipError_t as int.
 int launch_reduce(const KernelArgs& a, bool write_masks, hipStream_t s);
 // The optimised hot kernel (trik_hsv_stripe.hip); returns hipErrorNotSupported
 // when the geometry needs the generic kernel (misaligned input, width > 8192).
@@ -82,5 +108,16 @@ int launch_targets(const TrikHsvFrameBatch& b, int n_ranges, const TrikHsvTarget
                    TrikHsvTarget* targets, hipStream_t s);
 int launch_synth(const TrikHsvFrameBatch& b, uint8_t* frames, int first_frame, int kind,
                  uint64_t seed, hipStream_t s);
+// preview_kernel then overlay_kernel (circle from sums[f * sums_pitch])
+int launch_preview(const PreviewArgs& a, const TrikHsvTargetSums* sums, int sums_pitch, hipStream_t s);
+int launch_auto_range(const AutoRangeArgs& a, hipStream_t s);
+
+// Host side of the preview geometry (trik_hsv_tables.cpp): the reference's
+// scale maps and their inverses, packed as
+//   wi2wo[width], hi2ho[height], last_row[out_h], last_col[out_w]  (32-bit each).
+void preview_maps(int width, int height, int out_w, int out_h, uint32_t* maps);
+// Zone bounds of HsvRangeDetector::initImg (hpp:88-108) for zone scale 6.
+void auto_range_zone(int width, int height, int32_t& c_lo, int32_t& c_hi, int32_t& r_lo,
+                     int32_t& r_hi);
 
 }  // namespace trik_hsv

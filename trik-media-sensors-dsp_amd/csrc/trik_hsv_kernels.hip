@@ -16,38 +16,13 @@
 #include <hip/hip_runtime.h>
 
 #include "trik_hsv_internal.h"
+#include "trik_hsv_pixel.h"
 
 namespace trik_hsv {
 
 constexpr int kBlock = 512;           // 8 waves; 2 workgroups per CU (66 KB LDS each)
 constexpr int kBlocksPerCU = 2;
 constexpr int kTileChunks = 4096;     // 16-byte chunks (8 pixels) per tile, about 64 KB of YUYV
-
-// ---------------------------------------------------------------------------
-// Per-pixel arithmetic (equal to WSEQ:181-249 on all 2^24
-// inputs -- tests/test_gpu_parity.py checks this exhaustively on the device).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ int clamp8(int v) { return min(max(v, 0), 255); }
-
-// (Y,U,V) -> T-bit mask of the ranges whose H, S and V tests all pass.
-__device__ __forceinline__ uint32_t detect_pixel(int Y, int U, int V, const RangeTables& t) {
-  const int y74 = 74 * Y;
-  const int r = clamp8((102 * V + y74 - 14248) >> 6);                 // WSEQ:191-203
-  const int g = clamp8((-52 * V - 25 * U + y74 + 8696) >> 6);
-  const int b = clamp8(((int)(int16_t)(129 * U + y74 - 17672)) >> 6);  // _add2 wraps at 16 bits
-  const int mx = max(r, max(g, b));
-  const int mn = min(r, min(g, b));
-  const int m = t.lut43[mx - mn];                                      // WSEQ:227-228
-  int h;                                                               // WSEQ:230-242
-  if (mx == g)
-    h = 21845 + m * (b - r);
-  else if (mx == b)
-    h = 43690 + m * (r - g);
-  else
-    h = m * (g - b);
-  const uint32_t H = ((uint32_t)h >> 8) & 0xFFu;                       // WSEQ:244-247
-  return (uint32_t)t.hue[H] & (uint32_t)t.sv[(mx << 8) | mn];
-}
 
 template <int NR>
 struct Acc {

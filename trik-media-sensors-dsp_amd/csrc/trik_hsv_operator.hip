@@ -1,0 +1,233 @@
+// trik_hsv_operator.hip -- the operator's outputs besides the target sums
+// (SURVEY 8(f) rows 1 and 2), paths relative to the reference checkout, WSEQ
+// as in include/trik_hsv.h:
+//
+//  preview_kernel     the RGB565X preview stream written by proceedImageHsv
+//                     (WSEQ:316-354): every source pixel is written through the
+//                     truncated scale maps (WSEQ:371-387), last writer wins, a
+//                     detected pixel as 0x00ffff.  Computed as a gather: output
+//                     pixel (r', c') takes the last source row / column that
+//                     maps onto it (host-built inverse maps), never-written
+//                     output pixels keep the zero fill of WFXNS:234.
+//  overlay_kernel     the guide lines and target circle of WSEQ:66-166,471-494,
+//                     drawn in the reference's order by one lane per frame.
+//  auto_range_kernel  HsvRangeDetector::detect (trik/webcam/object_sensor/
+//                     include/internal/cv_hsv_range_detector.hpp:88-198; zone
+//                     scale 6, WSEQ:32,455-462): H, S and V histograms of the
+//                     central zone; the reference keeps the value whose count
+//                     first exceeds the running maximum in scan order.  A value
+//                     with the final maximum count M occurs exactly M times, so
+//                     its M-th occurrence is its last one: the winner is the
+//                     max-count value with the earliest last occurrence -- one
+//                     pass of LDS histograms plus atomicMax of scan positions.
+#include <hip/hip_runtime.h>
+
+#include "trik_hsv_internal.h"
+#include "trik_hsv_pixel.h"
+
+namespace trik_hsv {
+
+namespace {
+
+struct Luts {
+  uint16_t l43[256], l255[256];
+};
+constexpr Luts make_luts() {  // WSEQ:400-406
+  Luts l{};
+  for (uint32_t i = 1; i < 256; ++i) {
+    l.l43[i] = (uint16_t)((43u * 256u) / i);
+    l.l255[i] = (uint16_t)((255u * 256u) / i);
+  }
+  return l;
+}
+__constant__ Luts c_luts = make_luts();
+
+// writeOutputPixel, WSEQ:66-70: 0x00RRGGBB -> B5 G6 R5 (R in the low bits),
+// little-endian bytes (the output line length need not be even).
+__device__ __forceinline__ void write_px(uint8_t* dst, uint32_t rgb888) {
+  const uint32_t v = ((rgb888 >> 19) & 0x001fu) | ((rgb888 >> 5) & 0x07e0u) | ((rgb888 << 8) & 0xf800u);
+  dst[0] = (uint8_t)v;
+  dst[1] = (uint8_t)(v >> 8);
+}
+
+__global__ __launch_bounds__(256) void preview_kernel(PreviewArgs a) {
+  const int f = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)a.out_w * a.out_h) return;
+  const int r = (int)(i / a.out_w), c = (int)(i - (int64_t)r * a.out_w);
+  const int sr = a.last_row[r], sc = a.last_col[c];
+  if (sr < 0 || sc < 0) return;
+  const uint8_t* fr = a.frames + (int64_t)f * a.frame_stride;
+  int Y, U, V;
+  fetch_yuv(fr, a.height, a.line_length, a.layout, sr, sc, Y, U, V);
+  const PixelRgb p = pixel_rgb(Y, U, V);
+  const uint32_t det = detect_pixel(Y, U, V, *a.tables) & 1u;
+  write_px(a.previews + (int64_t)f * a.preview_stride + (int64_t)r * a.out_ll + 2 * c,
+           det ? 0x00ffffu : p.rgb888());
+}
+
+struct Canvas {
+  uint8_t* out;
+  int out_ll, width, height;
+  const uint32_t* wi2wo;
+  const uint32_t* hi2ho;
+  // drawOutputPixelBound, WSEQ:72-89 (source point clamped to the image)
+  __device__ void px(int32_t col, int32_t row, uint32_t rgb) const {
+    const int32_t sc = col < 0 ? 0 : (col > width - 1 ? width - 1 : col);
+    const int32_t sr = row < 0 ? 0 : (row > height - 1 ? height - 1 : row);
+    write_px(out + (int64_t)(int32_t)hi2ho[sr] * out_ll + (int64_t)(int32_t)wi2wo[sc] * 2, rgb);
+  }
+};
+
+__global__ void overlay_kernel(PreviewArgs a, const TrikHsvTargetSums* sums, int sums_pitch) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= a.n_frames) return;
+  const Canvas cv{a.previews + (int64_t)f * a.preview_stride, a.out_ll, a.width, a.height, a.wi2wo,
+                  a.hi2ho};
+  const int step = a.height / 6, hh = a.height / 2, hw = a.width / 2;  // WSEQ:471-474
+  const int32_t vcols[4] = {hw - 2 * step, hw - step, hw + step, hw + 2 * step};
+  for (int k = 0; k < 4; ++k)  // drawRgbTargetCenterLine, WSEQ:136-150
+    for (int adj = 0; adj < 100; ++adj) {
+      cv.px(vcols[k], hh - adj, 0xff00ff);
+      cv.px(vcols[k], hh + adj, 0xff00ff);
+    }
+  const int32_t hrows[4] = {hh - 2 * step, hh - step, hh + step, hh + 2 * step};
+  for (int k = 0; k < 4; ++k)  // drawRgbTargetHorizontalCenterLine, WSEQ:152-166
+    for (int adj = 0; adj < 100; ++adj) {
+      cv.px(hw - adj, hrows[k], 0xff00ff);
+      cv.px(hw + adj, hrows[k], 0xff00ff);
+    }
+  const TrikHsvTargetSums s = sums[(int64_t)f * sums_pitch];
+  const uint32_t n = (uint32_t)s.points;
+  if (n == 0) return;
+  // WSEQ:486-490 (as targets_kernel): unsigned division, IEEE fp32 radius
+  const int32_t cx = (int32_t)((uint32_t)(int32_t)s.sum_x / n);
+  const int32_t cy = (int32_t)((uint32_t)(int32_t)s.sum_y / n);
+  const int32_t radius = (int32_t)(uint32_t)ceilf(__fsqrt_rn(__fdiv_rn((float)n, 3.1415927f)));
+  // drawOutputCircle, WSEQ:91-134 (midpoint circle), colour 0xffff00
+  int32_t err = 1 - radius, err_y = 1, err_x = -2 * radius, x = radius, y = 0;
+  const uint32_t rgb = 0xffff00;
+  cv.px(cx, cy + radius, rgb);
+  cv.px(cx, cy - radius, rgb);
+  cv.px(cx + radius, cy, rgb);
+  cv.px(cx - radius, cy, rgb);
+  while (y < x) {
+    if (err >= 0) {
+      x -= 1;
+      err_x += 2;
+      err += err_x;
+    }
+    y += 1;
+    err_y += 2;
+    err += err_y;
+    cv.px(cx + x, cy + y, rgb);
+    cv.px(cx + x, cy - y, rgb);
+    cv.px(cx - x, cy + y, rgb);
+    cv.px(cx - x, cy - y, rgb);
+    cv.px(cx + y, cy + x, rgb);
+    cv.px(cx + y, cy - x, rgb);
+    cv.px(cx - y, cy + x, rgb);
+    cv.px(cx - y, cy - x, rgb);
+  }
+}
+
+constexpr int kRangeBlock = 256;
+
+// H, S, V bytes of one pixel (WSEQ:207-249) from the constant LUTs.
+__device__ __forceinline__ void hsv_bytes(const uint8_t* fr, const AutoRangeArgs& a, int row, int col,
+                                          uint32_t (&hsv)[3]) {
+  int Y, U, V;
+  fetch_yuv(fr, a.height, a.line_length, a.layout, row, col, Y, U, V);
+  const PixelRgb p = pixel_rgb(Y, U, V);
+  const int mx = max(p.r, max(p.g, p.b)), mn = min(p.r, min(p.g, p.b));
+  const int m = c_luts.l43[mx - mn];
+  int h;
+  if (mx == p.g) h = 21845 + m * (p.b - p.r);
+  else if (mx == p.b) h = 43690 + m * (p.r - p.g);
+  else h = m * (p.g - p.b);
+  hsv[0] = ((uint32_t)h >> 8) & 0xFFu;
+  hsv[1] = ((uint32_t)c_luts.l255[mx] * (uint32_t)(mx - mn)) >> 8;
+  hsv[2] = (uint32_t)mx;
+}
+
+__global__ __launch_bounds__(kRangeBlock) void auto_range_kernel(AutoRangeArgs a) {
+  __shared__ uint32_t cnt[3][256];
+  __shared__ uint32_t last[3][256];
+  __shared__ uint64_t best[3];
+  const int f = blockIdx.x;
+  for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) {
+    (&cnt[0][0])[i] = 0;
+    (&last[0][0])[i] = 0;
+  }
+  if (threadIdx.x < 3) best[threadIdx.x] = ~0ull;
+  __syncthreads();
+  // zone: c_lo < col < c_hi, r_lo < row < r_hi (uint16 bounds, hpp:88-108)
+  const int c0 = max(a.c_lo + 1, 0), c1 = min(a.c_hi, a.width);  // [c0, c1)
+  const int r0 = max(a.r_lo + 1, 0), r1 = min(a.r_hi, a.height);
+  const int zw = c1 - c0, zh = r1 - r0;
+  const uint8_t* fr = a.frames + (int64_t)f * a.frame_stride;
+  if (zw > 0 && zh > 0) {
+    for (int64_t i = threadIdx.x; i < (int64_t)zw * zh; i += blockDim.x) {
+      const int row = r0 + (int)(i / zw), col = c0 + (int)(i % zw);
+      uint32_t hv[3];
+      hsv_bytes(fr, a, row, col, hv);
+      const uint32_t pos = (uint32_t)((int64_t)row * a.width + col);  // scan order of s_rgb888hsv
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        atomicAdd(&cnt[k][hv[k]], 1u);
+        atomicMax(&last[k][hv[k]], pos);
+      }
+    }
+  }
+  __syncthreads();
+  // per channel: max count M, then the earliest last occurrence among count == M
+  // key = (~count) << 32 | last  ->  min key = max count, then min last
+  for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) {
+    const int k = i >> 8, v = i & 255;
+    const uint32_t c = cnt[k][v];
+    if (c) atomicMin(reinterpret_cast<unsigned long long*>(&best[k]),
+                     ((unsigned long long)(~c) << 32) | last[k][v]);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t win[3];
+    for (int k = 0; k < 3; ++k) {
+      win[k] = 0;  // no zone pixels: the reference keeps m_max* = 0
+      if (best[k] != ~0ull) {
+        const uint32_t pos = (uint32_t)best[k];
+        uint32_t hv[3];  // the winning value is the one at its last position
+        hsv_bytes(fr, a, (int)(pos / (uint32_t)a.width), (int)(pos % (uint32_t)a.width), hv);
+        win[k] = hv[k];
+      }
+    }
+    uint16_t* o = a.out + (int64_t)f * 6;  // hpp:190-195: float constants promoted to double
+    o[0] = (uint16_t)((double)win[0] * (double)1.4f);
+    o[1] = 15;
+    o[2] = (uint16_t)((double)win[1] * (double)0.39f);
+    o[3] = 30;
+    o[4] = (uint16_t)((double)win[2] * (double)0.39f);
+    o[5] = 30;
+  }
+}
+
+}  // namespace
+
+int launch_preview(const PreviewArgs& a, const TrikHsvTargetSums* sums, int sums_pitch, hipStream_t s) {
+  if (a.n_frames <= 0 || a.out_w <= 0 || a.out_h <= 0) return hipSuccess;
+  const int64_t px = (int64_t)a.out_w * a.out_h;
+  hipLaunchKernelGGL(preview_kernel, dim3((unsigned)((px + 255) / 256), (unsigned)a.n_frames), dim3(256),
+                     0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || a.width <= 0 || a.height <= 0) return e;
+  hipLaunchKernelGGL(overlay_kernel, dim3((unsigned)((a.n_frames + 63) / 64)), dim3(64), 0, s, a, sums,
+                     sums_pitch);
+  return hipGetLastError();
+}
+
+int launch_auto_range(const AutoRangeArgs& a, hipStream_t s) {
+  if (a.n_frames <= 0) return hipSuccess;
+  hipLaunchKernelGGL(auto_range_kernel, dim3((unsigned)a.n_frames), dim3(kRangeBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace trik_hsv

@@ -43,12 +43,12 @@ static inline bool outside(uint32_t x, uint32_t lo, uint32_t hi) { return x < lo
 void compile_tables(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTables* out) {
   memset(out, 0, sizeof(*out));
   out->lut43[0] = 0;
-  uint16_t lut255[256];
-  lut255[0] = 0;
+  out->lut255[0] = 0;
   for (uint32_t i = 1; i < 256; ++i) {  // WSEQ:400-406
     out->lut43[i] = (uint16_t)((43u * 256u) / i);
-    lut255[i] = (uint16_t)((255u * 256u) / i);
+    out->lut255[i] = (uint16_t)((255u * 256u) / i);
   }
+  const uint16_t* lut255 = out->lut255;
   for (int t = 0; t < n; ++t) {
     const PackedRange p = pack_range(ranges[t]);
     const uint8_t bit = (uint8_t)(1u << t);
@@ -80,6 +80,38 @@ void compile_stripe_tables(const RangeTables& base, int n, StripeTables* out) {
       out->rows[i][kM43RowOffset / 4 + b] = base.lut43[i];
     }
   }
+}
+
+void preview_maps(int width, int height, int out_w, int out_h, uint32_t* maps) {
+  // WSEQ:371-387: shift = min(out/in) in double, maps truncate i * shift
+  const double sw = width > 0 ? (double)out_w / width : 0.0;
+  const double sh = height > 0 ? (double)out_h / height : 0.0;
+  const double shift = sw < sh ? sw : sh;
+  uint32_t* wi2wo = maps;
+  uint32_t* hi2ho = wi2wo + width;
+  int32_t* last_row = reinterpret_cast<int32_t*>(hi2ho + height);
+  int32_t* last_col = last_row + out_h;
+  for (int i = 0; i < width; ++i) wi2wo[i] = (uint32_t)(i * shift);
+  for (int i = 0; i < height; ++i) hi2ho[i] = (uint32_t)(i * shift);
+  for (int i = 0; i < out_h; ++i) last_row[i] = -1;
+  for (int i = 0; i < out_w; ++i) last_col[i] = -1;
+  // scan order: a later source row/column overwrites (proceedImageHsv)
+  for (int i = 0; i < height; ++i)
+    if (hi2ho[i] < (uint32_t)out_h) last_row[hi2ho[i]] = i;
+  for (int i = 0; i < width; ++i)
+    if (wi2wo[i] < (uint32_t)out_w) last_col[wi2wo[i]] = i;
+}
+
+void auto_range_zone(int width, int height, int32_t& c_lo, int32_t& c_hi, int32_t& r_lo, int32_t& r_hi) {
+  // HsvRangeDetector::initImg (cv_hsv_range_detector.hpp:88-108), zone scale 6
+  // (WSEQ:32): uint16_t fields, so differences wrap modulo 2^16.
+  const uint16_t h_height = (uint16_t)((uint32_t)height / 2);
+  const uint16_t h_width = (uint16_t)((uint32_t)width / 2);
+  const uint16_t step = (uint16_t)((uint32_t)height / 6);
+  c_lo = (uint16_t)(h_width - step);
+  c_hi = (uint16_t)(h_width + step);
+  r_lo = (uint16_t)(h_height - step);
+  r_hi = (uint16_t)(h_height + step);
 }
 
 }  // namespace trik_hsv

@@ -141,6 +141,39 @@ class Detector:
             raise TrikHsvError(rc, "trik_hsv_batch_masks")
         return masks, sums
 
+    def batch_preview(self, frames, width, height, line_length, layout, hsv_range, sums, *,
+                      out_width=None, out_height=None, out_line_length=None, n_frames=None,
+                      frame_stride=None, sums_pitch=1, stream=None):
+        """RGB565X previews (uint8 [N, out_height, out_line_length]) for one range;
+        `sums` holds that range's per-frame sums (every `sums_pitch` entries)."""
+        import torch
+
+        b = _batch(frames, width, height, line_length, layout, n_frames, frame_stride)
+        ow = width // 2 if out_width is None else out_width
+        oh = height // 2 if out_height is None else out_height
+        oll = 2 * ow if out_line_length is None else out_line_length
+        previews = torch.empty((b.n_frames, oh, oll), dtype=torch.uint8, device=frames.device)
+        arr, _ = _ranges([hsv_range])
+        rc = _lib.trik_hsv_batch_preview(self._h, C.byref(b), arr, C.c_void_p(sums.data_ptr()),
+                                         sums_pitch, ow, oh, oll, C.c_void_p(previews.data_ptr()),
+                                         oh * oll, _stream_ptr(stream))
+        if rc:
+            raise TrikHsvError(rc, "trik_hsv_batch_preview")
+        return previews
+
+
+def batch_auto_range(frames, width, height, line_length, layout, *, n_frames=None,
+                     frame_stride=None, stream=None):
+    """autoDetectHsv per frame: uint16 [N, 6] = hue, hueTol, sat, satTol, val, valTol."""
+    import torch
+
+    b = _batch(frames, width, height, line_length, layout, n_frames, frame_stride)
+    out = torch.empty((b.n_frames, 6), dtype=torch.int16, device=frames.device)
+    rc = _lib.trik_hsv_batch_auto_range(C.byref(b), C.c_void_p(out.data_ptr()), _stream_ptr(stream))
+    if rc:
+        raise TrikHsvError(rc, "trik_hsv_batch_auto_range")
+    return out
+
 
 def batch_targets(sums, width, height, *, stream=None):
     """Epilogue only: sums int64 [N,T,3] -> targets int8 [N,T,4]."""

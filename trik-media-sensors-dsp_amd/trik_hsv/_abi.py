@@ -156,6 +156,9 @@ PROTOTYPES = {
                                 C.c_void_p], i32),
     "trik_hsv_batch_masks": ([C.c_void_p, C.POINTER(FrameBatch), C.POINTER(InArgsAlg), i32,
                               C.c_void_p, C.c_void_p, C.c_void_p], i32),
+    "trik_hsv_batch_preview": ([C.c_void_p, C.POINTER(FrameBatch), C.POINTER(InArgsAlg), C.c_void_p,
+                                i32, i32, i32, i32, C.c_void_p, C.c_int64, C.c_void_p], i32),
+    "trik_hsv_batch_auto_range": ([C.POINTER(FrameBatch), C.c_void_p, C.c_void_p], i32),
     "trik_hsv_synth": ([C.POINTER(FrameBatch), i32, i32, u64, C.c_void_p], i32),
 }
 
