@@ -1,0 +1,99 @@
+"""Measure the operator outputs of SURVEY 8(f) rows 1-2 on the C3 batch.
+
+  preview     trik_hsv_batch_preview: 4096 x 640x480 YUYV -> 320x240 RGB565X
+              previews for one range.  Algorithmic bytes per frame: the source
+              rows the 2:1 preview samples (H/2 rows of lineLength bytes) plus
+              the preview written (outH * outLineLength), read/written once.
+  auto_range  trik_hsv_batch_auto_range: the central zone of each frame
+              (159 x 159 px at 640x480, 2 B/px) -- small, launch/latency-bound.
+  process     one host frame through the XDAIS quartet (H2D + kernels + D2H,
+              PCIe-inclusive latency per frame), with preview and auto range.
+
+Prints one JSON object.  usage: python scripts/bench_operator.py [--frames N]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "trik-media-sensors-dsp_amd"))
+HBM_PEAK_GBS = 8000.0
+
+
+def timed(fn, stream, iters):
+    """Average GPU time per call of `iters` back-to-back calls (asynchronous
+    launches, so host-side call overhead overlaps the previous call's kernels)."""
+    import torch
+
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    for _ in range(iters):
+        fn()
+    b.record(stream)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=4096)
+    ap.add_argument("--iters", type=int, default=10)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+
+    import trik_hsv
+
+    W, H, LL, F = 640, 480, 1280, args.frames
+    OW, OH, OLL = 320, 240, 640
+    T0 = (0, 30, 50, 100, 30, 100)
+    dev = torch.empty(F * H * LL, dtype=torch.uint8, device="cuda")
+    trik_hsv.synth(dev, W, H, LL, trik_hsv.LAYOUT_YUYV, 1, 0x7A1C)
+    stream = torch.cuda.current_stream()
+    det = trik_hsv.Detector()
+    sums, _ = det.process_batch(dev, W, H, LL, trik_hsv.LAYOUT_YUYV, [T0])
+    out = {}
+
+    pv_ms = timed(lambda: det.batch_preview(dev, W, H, LL, trik_hsv.LAYOUT_YUYV, T0, sums,
+                                            out_width=OW, out_height=OH, out_line_length=OLL),
+                  stream, args.iters)
+    pv_bytes = F * ((H // 2) * LL + OH * OLL)
+    out["preview"] = {"frames": F, "ms": round(pv_ms, 4), "Mframes_per_s": round(F / pv_ms / 1e3, 3),
+                      "bytes_algorithmic": pv_bytes,
+                      "achieved_GBs": round(pv_bytes / (pv_ms / 1e3) / 1e9, 1),
+                      "hbm_frac": round(pv_bytes / (pv_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                      "note": "preview_kernel (writes every preview byte) + overlay_kernel"}
+
+    ar_ms = timed(lambda: trik_hsv.batch_auto_range(dev, W, H, LL, trik_hsv.LAYOUT_YUYV), stream,
+                  args.iters)
+    zone = 159 * 159
+    out["auto_range"] = {"frames": F, "ms": round(ar_ms, 4), "Mframes_per_s": round(F / ar_ms / 1e3, 3),
+                         "zone_px_per_frame": zone,
+                         "achieved_GBs": round(F * zone * 2 / (ar_ms / 1e3) / 1e9, 1)}
+
+    s = trik_hsv.ObjectSensor()
+    assert s.set_params(W, H, LL) == 0
+    host = dev[: H * LL].cpu().numpy()
+    prev = np.zeros(OH * OLL, np.uint8)
+    for _ in range(3):
+        s.process(host, T0, out_buffer=prev, auto_detect=True)
+    n = 50
+    t0 = time.perf_counter()
+    for _ in range(n):
+        rc, _ = s.process(host, T0, out_buffer=prev, auto_detect=True)
+        assert rc == 0
+    dt = (time.perf_counter() - t0) / n
+    out["process_single_frame"] = {"ms_per_frame": round(dt * 1e3, 4),
+                                   "note": "host frame in, preview + targets + detect* out; "
+                                           "PCIe-inclusive, one synchronous call per frame"}
+    s.close()
+    det.close()
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

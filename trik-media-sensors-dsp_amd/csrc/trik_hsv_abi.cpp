@@ -301,14 +301,19 @@ int32_t ensure_maps(TrikCvHandle* h, int w, int hgt, int ow, int oh, hipStream_t
   return 0;
 }
 
-PreviewArgs preview_args(const TrikCvHandle* h, const TrikHsvFrameBatch& b, int ow, int oh, int oll,
+PreviewArgs preview_args(const TrikCvHandle* h, const TrikHsvFrameBatch& b,
+                         const TRIK_VIDTRANSCODE_CV_InArgsAlg& range, int ow, int oh, int oll,
                          uint8_t* previews, int64_t stride) {
   PreviewArgs a;
   a.frames = static_cast<const uint8_t*>(b.frames);
   a.frame_stride = b.frame_stride;
   a.n_frames = b.n_frames;
   a.width = b.width; a.height = b.height; a.line_length = b.line_length; a.layout = b.layout;
-  a.tables = h->d_tables;
+  a.range = pack_range(range);
+  const auto al = [](int64_t v) { return (v & 3) == 0; };
+  a.aligned4 = al((int64_t)reinterpret_cast<uintptr_t>(b.frames)) && (b.n_frames <= 1 || al(b.frame_stride)) &&
+               al(b.line_length) && al((int64_t)reinterpret_cast<uintptr_t>(previews)) &&
+               (b.n_frames <= 1 || al(stride)) && al(oll);
   a.out_w = ow; a.out_h = oh; a.out_ll = oll;
   a.previews = previews;
   a.preview_stride = stride;
@@ -503,9 +508,8 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
           }
           r = ensure_maps(h, h->in_w, h->in_h, h->out_w, h->out_h, h->stream);
           if (r) return r;
-          HIP_TRY(hipMemsetAsync(h->d_preview, 0, pb, h->stream));
-          const PreviewArgs pa = preview_args(h, b, h->out_w, h->out_h, h->out_ll, h->d_preview,
-                                              (int64_t)pb);
+          const PreviewArgs pa = preview_args(h, b, in_args->alg, h->out_w, h->out_h, h->out_ll,
+                                              h->d_preview, (int64_t)pb);
           HIP_TRY(launch_preview(pa, h->d_sums, 1, h->stream));
           HIP_TRY(hipMemcpyAsync(out_ptr, h->d_preview, pb, hipMemcpyDeviceToHost, h->stream));
         }
@@ -628,14 +632,10 @@ extern "C" int32_t trik_hsv_batch_preview(TRIK_VIDTRANSCODE_CV_Handle h, const T
   hipStream_t s = static_cast<hipStream_t>(stream);
   std::lock_guard<std::mutex> lock(h->mu);
   if (b->n_frames == 0 || pb == 0) return 0;
-  HIP_TRY(hipMemset2DAsync(previews, (size_t)(b->n_frames > 1 ? preview_stride : pb), 0, (size_t)pb,
-                           (size_t)b->n_frames, s));  // WFXNS:234 zero fill
-  if (b->width == 0 || b->height == 0) return 0;
-  rc = ensure_tables(h, range, 1, s);
-  if (rc) return rc;
+  // the preview kernel writes every byte of each preview, zeros included (WFXNS:234)
   rc = ensure_maps(h, b->width, b->height, out_width, out_height, s);
   if (rc) return rc;
-  HIP_TRY(launch_preview(preview_args(h, *b, out_width, out_height, out_line_length, previews,
+  HIP_TRY(launch_preview(preview_args(h, *b, *range, out_width, out_height, out_line_length, previews,
                                       preview_stride), sums, sums_pitch, s));
   if (!h->tables_busy) HIP_TRY(hipEventCreateWithFlags(&h->tables_busy, hipEventDisableTiming));
   HIP_TRY(hipEventRecord(h->tables_busy, s));

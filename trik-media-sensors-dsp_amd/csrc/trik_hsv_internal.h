@@ -79,7 +79,8 @@ struct PreviewArgs {
   const uint8_t* frames;
   int64_t frame_stride;
   int32_t n_frames, width, height, line_length, layout;
-  const RangeTables* tables;  // range 0 of these tables is the preview's range
+  PackedRange range;          // the preview's range (WSEQ:425-445)
+  int32_t aligned4;           // frames, strides, line lengths and previews 4-byte aligned
   int32_t out_w, out_h, out_ll;
   uint8_t* previews;
   int64_t preview_stride;

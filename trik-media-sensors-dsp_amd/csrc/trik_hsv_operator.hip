@@ -7,10 +7,11 @@
 //                     truncated scale maps (WSEQ:371-387), last writer wins, a
 //                     detected pixel as 0x00ffff.  Computed as a gather: output
 //                     pixel (r', c') takes the last source row / column that
-//                     maps onto it (host-built inverse maps), never-written
-//                     output pixels keep the zero fill of WFXNS:234.
+//                     maps onto it (host-built inverse maps); never-written
+//                     output pixels and the line padding are written as zero
+//                     (the zero fill of WFXNS:234).
 //  overlay_kernel     the guide lines and target circle of WSEQ:66-166,471-494,
-//                     drawn in the reference's order by one lane per frame.
+//                     one wave per frame, lines before circle as the reference.
 //  auto_range_kernel  HsvRangeDetector::detect (trik/webcam/object_sensor/
 //                     include/internal/cv_hsv_range_detector.hpp:88-198; zone
 //                     scale 6, WSEQ:32,455-462): H, S and V histograms of the
@@ -50,20 +51,71 @@ __device__ __forceinline__ void write_px(uint8_t* dst, uint32_t rgb888) {
   dst[1] = (uint8_t)(v >> 8);
 }
 
-__global__ __launch_bounds__(256) void preview_kernel(PreviewArgs a) {
-  const int f = blockIdx.y;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int64_t)a.out_w * a.out_h) return;
-  const int r = (int)(i / a.out_w), c = (int)(i - (int64_t)r * a.out_w);
-  const int sr = a.last_row[r], sc = a.last_col[c];
-  if (sr < 0 || sc < 0) return;
-  const uint8_t* fr = a.frames + (int64_t)f * a.frame_stride;
-  int Y, U, V;
-  fetch_yuv(fr, a.height, a.line_length, a.layout, sr, sc, Y, U, V);
+// detectHsvPixel (WSEQ:171-179) for one packed range: per-byte "outside the
+// bounds" bits compared with the expected pattern (1 for a wrapped hue).
+__device__ __forceinline__ bool detect_packed(uint32_t H, uint32_t S, uint32_t V, const PackedRange& r) {
+  const uint32_t out = ((H < (r.from & 0xFFu)) | (H > (r.to & 0xFFu))) |
+                       (((S < ((r.from >> 8) & 0xFFu)) | (S > ((r.to >> 8) & 0xFFu))) << 1) |
+                       (((V < ((r.from >> 16) & 0xFFu)) | (V > ((r.to >> 16) & 0xFFu))) << 2);
+  return out == r.expect;
+}
+
+// One pixel of the preview: RGB565X of (det ? 0x00ffff : rgb888), WSEQ:347.
+__device__ __forceinline__ uint32_t preview_px(int Y, int U, int V, const PackedRange& range) {
   const PixelRgb p = pixel_rgb(Y, U, V);
-  const uint32_t det = detect_pixel(Y, U, V, *a.tables) & 1u;
-  write_px(a.previews + (int64_t)f * a.preview_stride + (int64_t)r * a.out_ll + 2 * c,
-           det ? 0x00ffffu : p.rgb888());
+  const int mx = max(p.r, max(p.g, p.b)), mn = min(p.r, min(p.g, p.b));
+  const int m = c_luts.l43[mx - mn];
+  int h;
+  if (mx == p.g) h = 21845 + m * (p.b - p.r);
+  else if (mx == p.b) h = 43690 + m * (p.r - p.g);
+  else h = m * (p.g - p.b);
+  const uint32_t H = ((uint32_t)h >> 8) & 0xFFu;
+  const uint32_t S = ((uint32_t)c_luts.l255[mx] * (uint32_t)(mx - mn)) >> 8;
+  const uint32_t rgb = detect_packed(H, S, (uint32_t)mx, range) ? 0x00ffffu : p.rgb888();
+  return ((rgb >> 19) & 0x001fu) | ((rgb >> 5) & 0x07e0u) | ((rgb << 8) & 0xf800u);
+}
+
+// A wave per output row (4 rows per workgroup, frame and row from the block
+// index), a lane per 4 output bytes (two pixels).  Every byte of the out_h x
+// out_ll preview is written -- pixels no source pixel maps to and the line
+// padding as zero -- so the zero fill of WFXNS:234 needs no memset.
+constexpr int kPreviewRows = 4;
+__global__ __launch_bounds__(64 * kPreviewRows) void preview_kernel(PreviewArgs a) {
+  const int groups = (a.out_h + kPreviewRows - 1) / kPreviewRows;
+  const int f = blockIdx.x / groups;
+  const int r = (blockIdx.x - f * groups) * kPreviewRows + threadIdx.y;
+  if (r >= a.out_h) return;
+  const int quads = (a.out_ll + 3) >> 2;  // 4-byte groups per output row
+  uint8_t* row = a.previews + (int64_t)f * a.preview_stride + (int64_t)r * a.out_ll;
+  const uint8_t* fr = a.frames + (int64_t)f * a.frame_stride;
+  const int sr = a.last_row[r];
+  for (int q = threadIdx.x; q < quads; q += 64) {
+  uint32_t v[2] = {0u, 0u};
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int c = 2 * q + k;
+    if (c >= a.out_w || sr < 0) continue;
+    const int sc = a.last_col[c];
+    if (sc < 0) continue;
+    int Y, U, V;
+    if (a.layout == TRIK_HSV_LAYOUT_YUYV && a.aligned4) {
+      const uint32_t w = *reinterpret_cast<const uint32_t*>(fr + (int64_t)sr * a.line_length + 4 * (sc >> 1));
+      Y = (w >> (16 * (sc & 1))) & 0xFF;
+      U = (w >> 8) & 0xFF;
+      V = w >> 24;
+    } else {
+      fetch_yuv(fr, a.height, a.line_length, a.layout, sr, sc, Y, U, V);
+    }
+    v[k] = preview_px(Y, U, V, a.range);
+  }
+  const int b0 = 4 * q;
+  if (a.aligned4 && b0 + 4 <= a.out_ll) {
+    *reinterpret_cast<uint32_t*>(row + b0) = v[0] | (v[1] << 16);
+  } else {
+    const uint8_t bytes[4] = {(uint8_t)v[0], (uint8_t)(v[0] >> 8), (uint8_t)v[1], (uint8_t)(v[1] >> 8)};
+    for (int k = 0; k < 4 && b0 + k < a.out_ll; ++k) row[b0 + k] = bytes[k];
+  }
+  }
 }
 
 struct Canvas {
@@ -79,38 +131,47 @@ struct Canvas {
   }
 };
 
-__global__ void overlay_kernel(PreviewArgs a, const TrikHsvTargetSums* sums, int sums_pitch) {
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= a.n_frames) return;
+// One wave per frame.  All guide-line pixels have one colour and all circle
+// pixels another, so within each phase the write order is immaterial; only
+// "lines before circle" (WSEQ:476-494) is kept, by the barrier.
+__global__ __launch_bounds__(64) void overlay_kernel(PreviewArgs a, const TrikHsvTargetSums* sums,
+                                                     int sums_pitch) {
+  const int f = blockIdx.x, lane = threadIdx.x;
   const Canvas cv{a.previews + (int64_t)f * a.preview_stride, a.out_ll, a.width, a.height, a.wi2wo,
                   a.hi2ho};
   const int step = a.height / 6, hh = a.height / 2, hw = a.width / 2;  // WSEQ:471-474
-  const int32_t vcols[4] = {hw - 2 * step, hw - step, hw + step, hw + 2 * step};
-  for (int k = 0; k < 4; ++k)  // drawRgbTargetCenterLine, WSEQ:136-150
-    for (int adj = 0; adj < 100; ++adj) {
-      cv.px(vcols[k], hh - adj, 0xff00ff);
-      cv.px(vcols[k], hh + adj, 0xff00ff);
+  // 8 lines x 100 offsets x 2 points: drawRgbTargetCenterLine (vertical,
+  // WSEQ:136-150) at 4 columns, ...HorizontalCenterLine (WSEQ:152-166) at 4 rows
+  for (int k = lane; k < 8 * 100; k += 64) {
+    const int line = k / 100, adj = k % 100, off = (line & 3) < 2 ? ((line & 3) - 2) : ((line & 3) - 1);
+    if (line < 4) {
+      const int32_t col = hw + off * step;
+      cv.px(col, hh - adj, 0xff00ff);
+      cv.px(col, hh + adj, 0xff00ff);
+    } else {
+      const int32_t row = hh + off * step;
+      cv.px(hw - adj, row, 0xff00ff);
+      cv.px(hw + adj, row, 0xff00ff);
     }
-  const int32_t hrows[4] = {hh - 2 * step, hh - step, hh + step, hh + 2 * step};
-  for (int k = 0; k < 4; ++k)  // drawRgbTargetHorizontalCenterLine, WSEQ:152-166
-    for (int adj = 0; adj < 100; ++adj) {
-      cv.px(hw - adj, hrows[k], 0xff00ff);
-      cv.px(hw + adj, hrows[k], 0xff00ff);
-    }
+  }
+  __syncthreads();
   const TrikHsvTargetSums s = sums[(int64_t)f * sums_pitch];
   const uint32_t n = (uint32_t)s.points;
-  if (n == 0) return;
+  if (n == 0 || lane >= 8) return;
   // WSEQ:486-490 (as targets_kernel): unsigned division, IEEE fp32 radius
   const int32_t cx = (int32_t)((uint32_t)(int32_t)s.sum_x / n);
   const int32_t cy = (int32_t)((uint32_t)(int32_t)s.sum_y / n);
   const int32_t radius = (int32_t)(uint32_t)ceilf(__fsqrt_rn(__fdiv_rn((float)n, 3.1415927f)));
-  // drawOutputCircle, WSEQ:91-134 (midpoint circle), colour 0xffff00
-  int32_t err = 1 - radius, err_y = 1, err_x = -2 * radius, x = radius, y = 0;
+  // drawOutputCircle, WSEQ:91-134 (midpoint circle), colour 0xffff00; lane
+  // o draws octant o of every step (and one of the four axis points)
   const uint32_t rgb = 0xffff00;
-  cv.px(cx, cy + radius, rgb);
-  cv.px(cx, cy - radius, rgb);
-  cv.px(cx + radius, cy, rgb);
-  cv.px(cx - radius, cy, rgb);
+  const int sx = (lane & 1) ? -1 : 1, sy = (lane & 2) ? -1 : 1;
+  const bool swap = (lane & 4) != 0;
+  if (lane < 4) {
+    const int32_t ax[4] = {0, 0, radius, -radius}, ay[4] = {radius, -radius, 0, 0};
+    cv.px(cx + ax[lane], cy + ay[lane], rgb);
+  }
+  int32_t err = 1 - radius, err_y = 1, err_x = -2 * radius, x = radius, y = 0;
   while (y < x) {
     if (err >= 0) {
       x -= 1;
@@ -120,14 +181,7 @@ __global__ void overlay_kernel(PreviewArgs a, const TrikHsvTargetSums* sums, int
     y += 1;
     err_y += 2;
     err += err_y;
-    cv.px(cx + x, cy + y, rgb);
-    cv.px(cx + x, cy - y, rgb);
-    cv.px(cx - x, cy + y, rgb);
-    cv.px(cx - x, cy - y, rgb);
-    cv.px(cx + y, cy + x, rgb);
-    cv.px(cx + y, cy - x, rgb);
-    cv.px(cx - y, cy + x, rgb);
-    cv.px(cx - y, cy - x, rgb);
+    cv.px(cx + sx * (swap ? y : x), cy + sy * (swap ? x : y), rgb);
   }
 }
 
@@ -214,13 +268,12 @@ __global__ __launch_bounds__(kRangeBlock) void auto_range_kernel(AutoRangeArgs a
 
 int launch_preview(const PreviewArgs& a, const TrikHsvTargetSums* sums, int sums_pitch, hipStream_t s) {
   if (a.n_frames <= 0 || a.out_w <= 0 || a.out_h <= 0) return hipSuccess;
-  const int64_t px = (int64_t)a.out_w * a.out_h;
-  hipLaunchKernelGGL(preview_kernel, dim3((unsigned)((px + 255) / 256), (unsigned)a.n_frames), dim3(256),
-                     0, s, a);
+  const int64_t blocks = (int64_t)a.n_frames * ((a.out_h + kPreviewRows - 1) / kPreviewRows);
+  if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(preview_kernel, dim3((unsigned)blocks), dim3(64, kPreviewRows), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || a.width <= 0 || a.height <= 0) return e;
-  hipLaunchKernelGGL(overlay_kernel, dim3((unsigned)((a.n_frames + 63) / 64)), dim3(64), 0, s, a, sums,
-                     sums_pitch);
+  hipLaunchKernelGGL(overlay_kernel, dim3((unsigned)a.n_frames), dim3(64), 0, s, a, sums, sums_pitch);
   return hipGetLastError();
 }
 
