@@ -33,26 +33,26 @@ struct PackedRange {
   uint32_t from, to, expect;
 };
 
-// Tables of the stripe kernel (trik_hsv_stripe.hip), staged in LDS.  Layout
-// chosen for LDS banking and cheap addressing: the two
-// small tables are replicated once per bank so a wave's random lookups are
-// conflict-free, interleaved in 256-byte rows so that both addresses are one
-// and/or of a value already in the high byte; the large table has rows padded
-// to 260 bytes so the bank rotates with mx.
+// Tables of the stripe kernel (trik_hsv_stripe.hip), staged in LDS.  Sized so
+// that two 1024-thread workgroups fit one CU (2 x 78,848 B of 160 KiB), i.e.
+// 8 waves per SIMD:
 //   sv[mx * 260 + mn] : T-bit (sat AND val) mask for max mx, min mn (offset 0,
-//                       so its address is one v_mad_u32_u24)
-//   row[i] = { hue[i] x 32 banks, m43[i] x 32 banks }   (dwords)
-//     hue[H] : byte-spread hue mask (range t -> bit 8t)
-//     m43[d] : s_mult43_div (WSEQ:389-407)
+//                       so its address is one v_mad_u32_u24); rows padded to
+//                       260 bytes so the bank rotates with mx
+//   hue[H][kHueCopies] : byte-spread hue mask (range t -> bit 8t)
+//   m43[d][kM43Copies] : s_mult43_div (WSEQ:389-407)
+// The two small tables are replicated and interleaved so that lane L reads
+// copy L % copies: a wave's random lookups spread over the LDS banks.
 constexpr int kSvStride = 260;
-constexpr int kBanks = 32;
+constexpr int kHueCopies = 8;
+constexpr int kM43Copies = 4;
 struct alignas(16) StripeTables {
   uint8_t sv[256 * kSvStride];
-  uint32_t rows[256][2 * kBanks];
+  uint32_t hue[256 * kHueCopies];
+  uint32_t m43[256 * kM43Copies];
 };
-static_assert(sizeof(StripeTables) == 66560 + 65536, "table layout");
-constexpr uint32_t kHueRowOffset = 0;    // bytes into a row
-constexpr uint32_t kM43RowOffset = 128;
+static_assert(sizeof(StripeTables) == 66560 + 256 * 4 * (kHueCopies + kM43Copies), "table layout");
+static_assert(2 * sizeof(StripeTables) <= 160 * 1024, "two workgroups per CU");
 
 PackedRange pack_range(const TRIK_VIDTRANSCODE_CV_InArgsAlg& r);
 void compile_tables(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTables* out);

@@ -69,6 +69,10 @@ __device__ __forceinline__ uint32_t lds_u8(uint32_t addr) { return *(lds_u8_ptr)
 // context, scripts/ubench/pixel_mix.hip), and the compiler schedules it and
 // enforces the v_dot4 / VCC wait states itself.
 struct Phase1 { uint32_t m43_addr, sv_addr, diff, base; };
+constexpr int log2i(int v) { return v <= 1 ? 0 : 1 + log2i(v / 2); }
+constexpr int kM43Shift = log2i(4 * kM43Copies);  // byte stride of one m43 entry's copies
+constexpr int kHueShift = log2i(4 * kHueCopies);
+static_assert((1 << kM43Shift) == 4 * kM43Copies && (1 << kHueShift) == 4 * kHueCopies, "pow2 copies");
 __device__ __forceinline__ int clamp8_shift6(uint32_t s) {
   const int x = ((int)(s << 16)) >> 22;  // bits 15:6, sign from 15 (v_bfe_i32)
   const int lo = x < 0 ? 0 : x;
@@ -83,7 +87,7 @@ __device__ __forceinline__ Phase1 phase1(uint32_t w, uint32_t wc, uint32_t m43_l
   const int mx = max(r, max(g, b));
   const int mn = min(r, min(g, b));
   Phase1 p;
-  p.m43_addr = ((uint32_t)(mx - mn) << 8) + m43_lane;
+  p.m43_addr = ((uint32_t)(mx - mn) << kM43Shift) + m43_lane;
   p.sv_addr = __umul24((uint32_t)mx, (uint32_t)kSvStride) + (uint32_t)mn;
   const bool eqG = mx == g, eqB = mx == b;
   const int dR = g - b, dG = b - r, dB = r - g;
@@ -101,7 +105,7 @@ __device__ __forceinline__ Phase1 phase1(uint32_t w, uint32_t wc, uint32_t m43_l
 __device__ __forceinline__ uint32_t phase2_addr(uint32_t m, const Phase1& p, uint32_t hue_lane) {
   uint32_t h;
   asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(h) : "v"(m), "v"(p.diff), "v"(p.base));
-  return (h & 0xFF00u) + hue_lane;
+  return (((h >> 8) & 0xFFu) << kHueShift) + hue_lane;
 }
 
 // Combine: spread sv's bit t to bit 8t (terms at t + 7s are disjoint for
@@ -130,7 +134,7 @@ __device__ __forceinline__ void wave_sums(uint32_t (&v)[N]) {
   for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x143, 0xC, 0xF, false);
 }
 
-// Wave-reduce the per-lane frame accumulators and add them to sums[frame].
+// Wave-reduce the per-lane accumulators of one tile and add them to sums[frame].
 template <int NR>
 __device__ __forceinline__ void flush_frame(uint32_t (&acc)[3 * NR], int frame, const KernelArgs& a) {
   wave_sums<3 * NR>(acc);
@@ -168,7 +172,8 @@ __device__ __forceinline__ uint32_t pack_bits(uint32_t e) {
 }
 
 template <int LAYOUT, int NR, bool MASKS>
-__global__ __launch_bounds__(kMaxBlock) void stripe_kernel(KernelArgs a, StripeGeom g) {
+__global__ __launch_bounds__(kMaxBlock) __attribute__((amdgpu_waves_per_eu(8)))
+void stripe_kernel(KernelArgs a, StripeGeom g) {
   {  // stage the tables at LDS address 0 (dynamic LDS, sizeof(StripeTables))
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     const u32x4* src = reinterpret_cast<const u32x4*>(a.stripe_tables);
@@ -179,8 +184,8 @@ __global__ __launch_bounds__(kMaxBlock) void stripe_kernel(KernelArgs a, StripeG
   __syncthreads();
 
   const int t = threadIdx.x;
-  const uint32_t hue_lane = (uint32_t)offsetof(StripeTables, rows) + kHueRowOffset + ((t & 31) << 2);
-  const uint32_t m43_lane = (uint32_t)offsetof(StripeTables, rows) + kM43RowOffset + ((t & 31) << 2);
+  const uint32_t hue_lane = (uint32_t)offsetof(StripeTables, hue) + ((t % kHueCopies) << 2);
+  const uint32_t m43_lane = (uint32_t)offsetof(StripeTables, m43) + ((t % kM43Copies) << 2);
   const bool active = t < g.k * g.cpr;
   const int col = active ? t % g.cpr : 0;
   const int ro = active ? t / g.cpr : 0;
@@ -191,17 +196,8 @@ __global__ __launch_bounds__(kMaxBlock) void stripe_kernel(KernelArgs a, StripeG
 
   const int64_t t_begin = g.n_tiles * blockIdx.x / gridDim.x;
   const int64_t t_end = g.n_tiles * (blockIdx.x + 1) / gridDim.x;
-  // per-lane 32-bit sums of the current frame: {N, sumX, sumY} per range
-  uint32_t acc[3 * NR];
-#pragma unroll
-  for (int v = 0; v < 3 * NR; ++v) acc[v] = 0;
-  int cur = t_begin < t_end ? (int)(t_begin / g.tiles_per_frame) : -1;
   for (int64_t tile = t_begin; tile < t_end; ++tile) {
     const int f = (int)(tile / g.tiles_per_frame);
-    if (f != cur) {  // uniform across the workgroup
-      flush_frame<NR>(acc, cur, a);
-      cur = f;
-    }
     const int r0 = (int)(tile - (int64_t)f * g.tiles_per_frame) * g.k * g.steps;
     const int y0 = r0 + ro;
     // steps that hold at least one valid row of this tile (uniform per block)
@@ -220,46 +216,45 @@ __global__ __launch_bounds__(kMaxBlock) void stripe_kernel(KernelArgs a, StripeG
     uint32_t P0 = 0, P1 = 0, P2 = 0, P3 = 0, O = 0, Q = 0, CumS = 0;
     uint32_t Qa = 0, Qb = 0, Ba = 0, Bb = 0;
     int nb = 0;
-    // Software pipeline, two rows ahead.  Loads are unconditional (a row past
-    // the frame end re-reads the tile's first row) so the compiler can wait
-    // with a counted vmcnt instead of draining every load each step.
+    // Software pipeline, one row ahead (8 waves per SIMD hide the rest).
+    // Loads are unconditional (a row past the frame end re-reads the tile's
+    // first row) so the compiler can wait with a counted vmcnt.
     const uint8_t* pf = active ? p : a.frames + (int64_t)f * a.frame_stride;
     const int vsteps = active ? min(steps, (a.height - y0 + g.k - 1) / g.k) : 0;  // valid steps, this lane
-    // one step: 8 pixels of row y0 + s*k from the chunk words in `cw`
-    auto step = [&](const uint32_t (&cw)[4], int s) {
+    // 4 pixels (words w0, w1) of row y0 + s*k at chunk pixel offset 4*half
+    auto half_step = [&](uint32_t w0, uint32_t w1, int s, int half, uint32_t& Pa, uint32_t& Pb) {
       const bool valid = s < vsteps;
-      Phase1 p[8];
-      uint32_t m[8], sv[8], e[8];
+      Phase1 p[4];
+      uint32_t m[4], sv[4], e[4];
+      p[0] = phase1<0>(w0, w0 ^ 0xFF00FF00u, m43_lane);
+      p[1] = phase1<1>(w0, w0 ^ 0xFF00FF00u, m43_lane);
+      p[2] = phase1<0>(w1, w1 ^ 0xFF00FF00u, m43_lane);
+      p[3] = phase1<1>(w1, w1 ^ 0xFF00FF00u, m43_lane);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t wc = cw[q] ^ 0xFF00FF00u;
-        p[2 * q] = phase1<0>(cw[q], wc, m43_lane);
-        p[2 * q + 1] = phase1<1>(cw[q], wc, m43_lane);
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < 4; ++j) {
         m[j] = lds_u32(p[j].m43_addr);
         sv[j] = lds_u8(p[j].sv_addr);
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) e[j] = combine(lds_u32(phase2_addr(m[j], p[j], hue_lane)), sv[j]);
+      for (int j = 0; j < 4; ++j) e[j] = combine(lds_u32(phase2_addr(m[j], p[j], hue_lane)), sv[j]);
       if (MASKS && valid) {
         const int y = y0 + s * g.k;
-        uint8_t* mp = a.masks + ((int64_t)f * a.height + y) * a.width + x0;
+        uint8_t* mp = a.masks + ((int64_t)f * a.height + y) * a.width + x0 + 4 * half;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < 4; ++j) {
           const uint8_t bits = (uint8_t)(pack_bits(e[j]) << a.mask_shift);
           mp[j] = a.mask_shift ? (uint8_t)(mp[j] | bits) : bits;
         }
       }
       if (valid) {  // false only for rows past the frame end and idle lanes
-        P0 = P0 + e[0] + e[1];
-        P1 = P1 + e[2] + e[3];
-        P2 = P2 + e[4] + e[5];
-        P3 = P3 + e[6] + e[7];
+        Pa = Pa + e[0] + e[1];
+        Pb = Pb + e[2] + e[3];
         O = O + e[1] + e[3];
-        O = O + e[5] + e[7];
       }
+    };
+    auto step = [&](const uint32_t (&cw)[4], int s) {
+      half_step(cw[0], cw[1], s, 0, P0, P1);
+      half_step(cw[2], cw[3], s, 1, P2, P3);
       Q = Q + P0 + P1;
       Q = Q + P2 + P3;
       ++nb;
@@ -275,24 +270,20 @@ __global__ __launch_bounds__(kMaxBlock) void stripe_kernel(KernelArgs a, StripeG
       }
     };
     auto row_ptr = [&](int s) { return s < vsteps ? pf + (int64_t)s * rowstep : pf; };
-    // three buffers rotate statically (unroll by 3): two rows stay in flight
-    uint32_t wa[4], wb[4], wc3[4];
+    uint32_t wa[4], wb[4];  // two buffers rotate statically (unroll by 2)
     load_chunk<LAYOUT>(row_ptr(0), plane, wa);
-    load_chunk<LAYOUT>(row_ptr(1), plane, wb);
-    for (int s = 0; s < steps; s += 3) {
-      load_chunk<LAYOUT>(row_ptr(s + 2), plane, wc3);
+    for (int s = 0; s < steps; s += 2) {
+      load_chunk<LAYOUT>(row_ptr(s + 1), plane, wb);
       step(wa, s);
       if (s + 1 >= steps) break;
-      load_chunk<LAYOUT>(row_ptr(s + 3), plane, wa);
+      load_chunk<LAYOUT>(row_ptr(s + 2), plane, wa);
       step(wb, s + 1);
-      if (s + 2 >= steps) break;
-      load_chunk<LAYOUT>(row_ptr(s + 4), plane, wb);
-      step(wc3, s + 2);
     }
     Qa += Ba;  // sum over steps of the cumulative count, 16-bit fields
     Qb += Bb;
 
-    // unpack per range into the frame accumulators
+    // unpack per range, wave-reduce, one atomic per value per wave and tile
+    uint32_t acc[3 * NR];
     const uint32_t C = P0 + P1 + P2 + P3;
 #pragma unroll
     for (int rr = 0; rr < NR; ++rr) {
@@ -301,13 +292,13 @@ __global__ __launch_bounds__(kMaxBlock) void stripe_kernel(KernelArgs a, StripeG
       const uint32_t wx = 2u * ((P1 >> sh) & 0xFFu) + 4u * ((P2 >> sh) & 0xFFu) +
                           6u * ((P3 >> sh) & 0xFFu) + ((O >> sh) & 0xFFu);
       const uint32_t qq = ((rr & 1) ? (Qb >> ((rr >> 1) * 16)) : (Qa >> ((rr >> 1) * 16))) & 0xFFFFu;
-      acc[3 * rr + 0] += c;
-      acc[3 * rr + 1] += x0 * c + wx;
+      acc[3 * rr + 0] = c;
+      acc[3 * rr + 1] = x0 * c + wx;
       // sum over steps of (y0 + k*s) * c_s = y0*C + k*(steps*C - sum of prefix counts)
-      acc[3 * rr + 2] += (uint32_t)y0 * c + (uint32_t)g.k * ((uint32_t)steps * c - qq);
+      acc[3 * rr + 2] = (uint32_t)y0 * c + (uint32_t)g.k * ((uint32_t)steps * c - qq);
     }
+    flush_frame<NR>(acc, f, a);
   }
-  if (cur >= 0) flush_frame<NR>(acc, cur, a);
 }
 
 bool geometry(const KernelArgs& a, StripeGeom& g) {
@@ -346,7 +337,8 @@ int launch_t(const KernelArgs& a, const StripeGeom& g, hipStream_t s) {
   static int cus = 0;
   if (!cus) cus = cu_count_stripe();
   const int block = ((g.k * g.cpr + 63) / 64) * 64;
-  const int64_t grid = g.n_tiles < cus ? g.n_tiles : cus;
+  const int64_t slots = 2LL * cus;  // two workgroups per CU (LDS and VGPR budgets)
+  const int64_t grid = g.n_tiles < slots ? g.n_tiles : slots;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(block), sizeof(StripeTables), s, a, g);
   return hipGetLastError();
 }

@@ -75,10 +75,8 @@ void compile_stripe_tables(const RangeTables& base, int n, StripeTables* out) {
   for (int i = 0; i < 256; ++i) {
     uint32_t spread = 0;
     for (int t = 0; t < n && t < 4; ++t) spread |= ((uint32_t)(base.hue[i] >> t) & 1u) << (8 * t);
-    for (int b = 0; b < kBanks; ++b) {
-      out->rows[i][kHueRowOffset / 4 + b] = spread;
-      out->rows[i][kM43RowOffset / 4 + b] = base.lut43[i];
-    }
+    for (int c = 0; c < kHueCopies; ++c) out->hue[i * kHueCopies + c] = spread;
+    for (int c = 0; c < kM43Copies; ++c) out->m43[i * kM43Copies + c] = base.lut43[i];
   }
 }
 

@@ -173,7 +173,10 @@ def load() -> C.CDLL:
             raise ImportError(f"{LIB_PATH} is missing: build it with `make -C {CSRC}` "
                               "(or __graft_entry__.build()); there is no CPU fallback")
         L = C.CDLL(LIB_PATH)
+        dev_override = bool(os.environ.get("TRIK_HSV_LIB"))
         for name, (args, res) in PROTOTYPES.items():
+            if dev_override and not hasattr(L, name):
+                continue  # older library under A/B: only what it exports
             fn = getattr(L, name)
             fn.argtypes, fn.restype = args, res
         _lib = L
