@@ -238,6 +238,19 @@ typedef struct TrikCvHandle* TRIK_VIDTRANSCODE_CV_Handle;
 int32_t TRIK_VIDTRANSCODE_CV_create(const TRIK_VIDTRANSCODE_CV_Params* params,
                                     TRIK_VIDTRANSCODE_CV_Handle* out_handle);
 
+/* The same quartet for the ov7670 line sensor's codec (its own DSP server in
+ * the reference: trik/ov7670/line_sensor, LineDetector<YUV422P, RGB565X> of
+ * include/internal/cv_line_detector_seqpass.hpp -- LSEQ below).  params ==
+ * NULL takes that glue's defaults (YUV422P in, RGB565X out; default dynamic
+ * output 240 wide x 320 high as its src/vidtranscode_cv.cpp:214,218).
+ * control/process/delete are the functions below; process() then runs
+ * LineDetector::run (LSEQ:376-476): V-range detection in columns 5..W-5,
+ * cross points over rows H/2..H/2+80, its preview overlays; OutArgs.targetY
+ * is the cross size.  autoDetectHsv is ignored (the line sensor's detector is
+ * seeded by srand(time(NULL))). */
+int32_t TRIK_VIDTRANSCODE_CV_create_line(const TRIK_VIDTRANSCODE_CV_Params* params,
+                                         TRIK_VIDTRANSCODE_CV_Handle* out_handle);
+
 /* Replaces TRIK_VIDTRANSCODE_CV_free (WFXNS:114-136). */
 int32_t TRIK_VIDTRANSCODE_CV_delete(TRIK_VIDTRANSCODE_CV_Handle handle);
 
@@ -352,6 +365,22 @@ int32_t trik_hsv_batch_preview(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsv
  * detectHueTolerance, detectSat, detectSatTolerance, detectVal,
  * detectValTolerance (uint16), as OutArgsAlg receives them. */
 int32_t trik_hsv_batch_auto_range(const TrikHsvFrameBatch* batch, uint16_t* out_dev, void* hip_stream);
+
+/* The line sensor for N ov7670 frames: sums_dev[i] =
+ * {points, sum_x, cross points} -- cross points in the sum_y slot -- for V in
+ * [val_from, val_to] (InArgs percent units) in columns 5..W-5, cross points
+ * over rows band_start..band_stop (the reference: H/2 .. H/2+80);
+ * targets_dev[i] (may be NULL) = OutArgs of LSEQ:455-474. */
+int32_t trik_hsv_line_batch(const TrikHsvFrameBatch* batch, int32_t val_from, int32_t val_to,
+                            int32_t band_start, int32_t band_stop, TrikHsvTargetSums* sums_dev,
+                            TrikHsvTarget* targets_dev, void* hip_stream);
+
+/* The line sensor's preview for N frames (window columns, guide, band and
+ * target lines, LSEQ:283-291, 433-467), from sums_dev of trik_hsv_line_batch. */
+int32_t trik_hsv_line_preview(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvFrameBatch* batch,
+                              int32_t val_from, int32_t val_to, const TrikHsvTargetSums* sums_dev,
+                              int32_t out_width, int32_t out_height, int32_t out_line_length,
+                              uint8_t* previews_dev, int64_t preview_stride, void* hip_stream);
 
 /* Fill batch->frames (device, writable) with synthetic frames; frame i of the
  * batch is global frame first_frame + i.  kind 0 = uniform random bytes,

@@ -95,6 +95,10 @@ def lib():
                                       C.POINTER(Range), C.c_int, C.c_int, C.c_int, C.c_int, vp,
                                       i64, C.POINTER(OutArgs)]
         L.trik_oracle_run.restype = C.c_int
+        L.trik_oracle_line_run.argtypes = [vp, i64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                           vp, C.c_int, C.c_int, C.c_int, vp, i64,
+                                           C.POINTER(OutArgs), vp]
+        L.trik_oracle_line_run.restype = C.c_int
         _lib = L
     return _lib
 
@@ -204,3 +208,43 @@ def run(frame_u8: np.ndarray, width, height, line_length, layout, rng, auto_dete
                                out.size if out is not None else 0, C.byref(oa))
     d = {k: getattr(oa, k) for k, _ in OutArgs._fields_}
     return rc, d, (out[:oh * oll] if out is not None else None)
+
+
+def line_run(frame_u8: np.ndarray, width, height, line_length, val_from, val_to, band=None,
+             out_width=None, out_height=None, out_line_length=None, preview=True):
+    """LineDetector::setup + run (ov7670 line sensor) for one frame.
+
+    band: (hStart, hStop) left by the previous run (default: the steady state
+    H/2, H/2+80).  Returns (rc, outargs dict, preview or None, sums[3], band_out)."""
+    fr = np.ascontiguousarray(frame_u8, dtype=np.uint8)
+    ow = width // 2 if out_width is None else out_width
+    oh = height // 2 if out_height is None else out_height
+    oll = 2 * ow if out_line_length is None else out_line_length
+    out = np.zeros(max(1, oh * oll), np.uint8) if preview else None
+    b = np.array(band if band is not None else (height // 2, height // 2 + 80), np.int32)
+    sums = np.zeros(3, np.int64)
+    oa = OutArgs()
+    rc = lib().trik_oracle_line_run(_ptr(fr), fr.size, width, height, line_length, val_from, val_to,
+                                    _ptr(b), ow, oh, oll, _ptr(out) if out is not None else None,
+                                    out.size if out is not None else 0, C.byref(oa), _ptr(sums))
+    d = {k: getattr(oa, k) for k, _ in OutArgs._fields_}
+    return rc, d, (out[:oh * oll] if out is not None else None), sums, tuple(int(v) for v in b)
+
+
+def line_scene(width, height, line_length, seed, x0=None, slope=0.25, line_w=24) -> np.ndarray:
+    """A test ov7670 (YUV422P) frame for the line sensor: a bright textured
+    floor with a dark slanted line, random bytes in the row padding (inputs for
+    the parity tests; not a reference fixture)."""
+    rng = np.random.default_rng(seed)
+    fr = rng.integers(0, 256, 2 * height * line_length, dtype=np.uint8)
+    y = fr[: height * line_length].reshape(height, line_length)
+    c = fr[height * line_length:].reshape(height, line_length)
+    y[:, :width] = rng.integers(150, 230, (height, width))
+    c[:, :width] = rng.integers(108, 148, (height, width))
+    x0 = width // 2 if x0 is None else x0
+    for r in range(height):
+        a = int(x0 + slope * (r - height / 2))
+        lo, hi = max(0, a), min(width, a + line_w)
+        if lo < hi:
+            y[r, lo:hi] = rng.integers(10, 50, hi - lo)
+    return fr

@@ -696,3 +696,95 @@ int trik_oracle_run(const uint8_t* frame, int64_t frame_size, int width, int hei
   free(img);
   return 0;
 }
+
+/* ------------------------------------------------------------------------ */
+/* ov7670 line sensor (LSEQ = trik/ov7670/line_sensor/include/internal/      */
+/* cv_line_detector_seqpass.hpp).                                            */
+/* ------------------------------------------------------------------------ */
+
+int trik_oracle_line_run(const uint8_t* frame, int64_t frame_size, int width, int height,
+                         int line_length, int val_from, int val_to, int32_t band[2],
+                         int out_width, int out_height, int out_line_length, uint8_t* out,
+                         int64_t out_size, trik_oracle_outargs* oa, int64_t sums[3]) {
+  enum { kStep = 40 }; /* LSEQ:422 */
+  memset(oa, 0, sizeof *oa);
+  if (width < 0 || height < 0 || width % 32 != 0 || height % 4 != 0) return -1; /* LSEQ:328-332 */
+  if (2LL * height * line_length > frame_size) return -1; /* both planes (LSEQ:378, :211-214) */
+  if (out && (int64_t)out_height * out_line_length > out_size) return -1;        /* LSEQ:380 */
+
+  const double sw = (double)out_width / width, sh = (double)out_height / height;
+  const double shift = sw < sh ? sw : sh; /* LSEQ:334-348 */
+  uint32_t* wi2wo = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(width > 0 ? width : 1));
+  uint32_t* hi2ho = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(height > 0 ? height : 1));
+  if (!wi2wo || !hi2ho) {
+    free(wi2wo); free(hi2ho);
+    return -1;
+  }
+  for (int i = 0; i < width; ++i) wi2wo[i] = (uint32_t)(i * shift);
+  for (int i = 0; i < height; ++i) hi2ho[i] = (uint32_t)(i * shift);
+
+  /* LSEQ:391-414: H and S bounds 0..255 unscaled, V scaled as the object sensor */
+  trik_oracle_range r = {0, 359, 0, 100, (uint8_t)val_from, (uint8_t)val_to};
+  uint32_t from, to, expect;
+  trik_oracle_pack_range(&r, &from, &to, &expect);
+  from = (from & 0x00FF0000u); /* H from 0, S from 0 */
+  to = (to & 0x00FF0000u) | 0x0000FFFFu;
+  expect = 0;
+
+  int32_t tx = 0;
+  uint32_t tn = 0, cross = 0;
+  const run_ctx ctx = {width, height, out_line_length, wi2wo, hi2ho, out};
+  if (height > 0 && width > 0) {
+    for (int row = 0; row < height; ++row) { /* convertImageYuyvToHsv + proceedImageHsv */
+      uint32_t row_n = 0, row_x = 0;
+      for (int q = 0; q < width / 2; ++q) {
+        uint32_t rgb[2];
+        trik_oracle_pair_rgb_c64x(pair_word(frame, height, line_length, TRIK_ORACLE_LAYOUT_OV7670, row, q), rgb);
+        for (int k = 0; k < 2; ++k) {
+          const int col = 2 * q + k;
+          if (col >= 5 && col <= width - 5) { /* LSEQ:288 */
+            const int det = trik_oracle_detect(trik_oracle_hsv_c64x(rgb[k]), from, to, expect);
+            row_n += (uint32_t)det;
+            row_x += det ? (uint32_t)col : 0;
+            if (out)
+              write_px(out + (int64_t)hi2ho[row] * out_line_length + (int64_t)wi2wo[col] * 2,
+                       det ? 0x00ffffu : rgb[k]);
+          }
+        }
+      }
+      tx += (int32_t)row_x;
+      tn += row_n;
+      if ((uint32_t)row >= (uint32_t)band[0] && (uint32_t)row <= (uint32_t)band[1]) cross += row_n;
+    }
+  }
+  const int h_width = width / 2, h_height = height / 2;
+  const int32_t draw_y = 0; /* m_inImageFirstRow - H/2 + H/2 with scale coefficient 1 */
+  if (out && width > 0 && height > 0) {
+    const int32_t cols[4] = {h_width - kStep, h_width + kStep, h_width - 2 * kStep, h_width + 2 * kStep};
+    for (int k = 0; k < 4; ++k) /* drawRgbThinLine, LSEQ:104-116 */
+      for (int adj = 0; adj < height; ++adj) draw_bound(&ctx, cols[k], draw_y + adj, 0xff00ff);
+  }
+  band[0] = h_height; /* LSEQ:449-450 */
+  band[1] = h_height + 2 * kStep;
+  const int cross_size = width > 0 ? (int)((uint32_t)(cross * 100u) / (uint32_t)(width * 2 * kStep)) : 0;
+  if (out && width > 0 && height > 0)
+    for (int k = 0; k < 2; ++k) /* drawRgbHorizontalLine, LSEQ:118-130 */
+      for (int adj = 0; adj < width; ++adj) draw_bound(&ctx, adj, band[k], 0xff0000);
+  if (tn > 10) { /* LSEQ:462-474 */
+    const int32_t cx = (int32_t)((uint32_t)tx / tn);
+    if (out)
+      for (int adj = 0; adj < height; ++adj) /* drawRgbTargetCenterLine, LSEQ:88-102 */
+        for (int d = -1; d <= 1; ++d) draw_bound(&ctx, cx + d, draw_y + adj, 0xff0000);
+    oa->target_x = (int8_t)(((cx - width / 2) * 100 * 2) / width);
+    oa->target_y = (int8_t)cross_size;
+    oa->target_size = (uint8_t)((uint32_t)(tn * 100u) / (uint32_t)(height * width));
+  }
+  if (sums) {
+    sums[0] = (int64_t)tn;
+    sums[1] = (int64_t)tx;
+    sums[2] = (int64_t)cross;
+  }
+  free(wi2wo);
+  free(hi2ho);
+  return 0;
+}

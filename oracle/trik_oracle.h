@@ -145,6 +145,28 @@ int      trik_oracle_run(const uint8_t* frame, int64_t frame_size, int width, in
                          int auto_detect, int out_width, int out_height, int out_line_length,
                          uint8_t* out, int64_t out_size, trik_oracle_outargs* oa);
 
+/* The ov7670 line sensor, LineDetector::setup + run (trik/ov7670/line_sensor/
+ * include/internal/cv_line_detector_seqpass.hpp:258-301, 376-476; LSEQ):
+ *   - the object sensor's per-pixel HSV on the ov7670 planes;
+ *   - detection by V only (hue and saturation bounds fixed at 0..255,
+ *     LSEQ:391-396), in columns 5 <= col <= W-5 only (LSEQ:288);
+ *   - cross points: detected pixels of rows hStart..hStop, where hStart and
+ *     hStop are the values the PREVIOUS run left (LSEQ:298 reads them before
+ *     LSEQ:449-450 sets them to H/2 and H/2+80); *band is that state, in and
+ *     out (the reference leaves it uninitialised before the first run);
+ *   - preview writes for the window columns only, thin guide lines, the two
+ *     band lines and the 3-pixel target line (LSEQ:433-463);
+ *   - OutArgs: targetX as the object sensor, targetY = cross points * 100 /
+ *     (W * 80), targetSize = N * 100 / (W * H), all 0 unless N > 10.
+ * autoDetectHsv is not restated: the line sensor's detector is a simulated
+ * annealing seeded by srand(time(NULL)) (cv_hsv_range_detector.hpp there),
+ * so its output is not reproducible; detect* are left untouched.
+ * sums (optional) receives {N, sumX, crossPoints}. */
+int      trik_oracle_line_run(const uint8_t* frame, int64_t frame_size, int width, int height,
+                              int line_length, int val_from, int val_to, int32_t band[2],
+                              int out_width, int out_height, int out_line_length, uint8_t* out,
+                              int64_t out_size, trik_oracle_outargs* oa, int64_t sums[3]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -6,6 +6,9 @@
               the preview written (outH * outLineLength), read/written once.
   auto_range  trik_hsv_batch_auto_range: the central zone of each frame
               (159 x 159 px at 640x480, 2 B/px) -- small, launch/latency-bound.
+  line        trik_hsv_line_batch: 4096 x 640x480 ov7670 (YUV422P) frames, the
+              line sensor's sums + OutArgs; algorithmic bytes = both planes
+              (2 B/px) once.  line_preview: its 320x240 previews.
   process     one host frame through the XDAIS quartet (H2D + kernels + D2H,
               PCIe-inclusive latency per frame), with preview and auto range.
 
@@ -74,6 +77,25 @@ def main():
     out["auto_range"] = {"frames": F, "ms": round(ar_ms, 4), "Mframes_per_s": round(F / ar_ms / 1e3, 3),
                          "zone_px_per_frame": zone,
                          "achieved_GBs": round(F * zone * 2 / (ar_ms / 1e3) / 1e9, 1)}
+
+    lf = min(F, 4096)
+    lfb = 2 * H * W
+    ldev = torch.empty(lf * lfb, dtype=torch.uint8, device="cuda")
+    trik_hsv.synth(ldev, W, H, W, trik_hsv.LAYOUT_OV7670, 1, 0x7A1C)
+    ln_ms = timed(lambda: trik_hsv.line_batch(ldev, W, H, W, 0, 30), stream, args.iters)
+    out["line"] = {"frames": lf, "ms": round(ln_ms, 4), "Mframes_per_s": round(lf / ln_ms / 1e3, 3),
+                   "bytes_algorithmic": lf * lfb,
+                   "achieved_GBs": round(lf * lfb / (ln_ms / 1e3) / 1e9, 1),
+                   "hbm_frac": round(lf * lfb / (ln_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                   "note": "line_sums_kernel + line_targets_kernel"}
+    lsums, _ = trik_hsv.line_batch(ldev, W, H, W, 0, 30)
+    lp_ms = timed(lambda: det.line_preview(ldev, W, H, W, 0, 30, lsums, out_width=OW, out_height=OH,
+                                           out_line_length=OLL), stream, args.iters)
+    lp_bytes = lf * (H // 2 * 2 * W + OH * OLL)
+    out["line_preview"] = {"frames": lf, "ms": round(lp_ms, 4),
+                           "achieved_GBs": round(lp_bytes / (lp_ms / 1e3) / 1e9, 1),
+                           "hbm_frac": round(lp_bytes / (lp_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+    del ldev
 
     s = trik_hsv.ObjectSensor()
     assert s.set_params(W, H, LL) == 0

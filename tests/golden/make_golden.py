@@ -67,6 +67,17 @@ RUN_CASES = [
     ("run_empty_point_no_circle", 320, 240, 640, O.LAYOUT_YUYV, 1, 3, 1, "empty_point", 1, 160, 120, 320),
 ]
 
+# ov7670 line sensor (LSEQ:376-476): (name, w, h, ll, scene seed, x0, slope,
+# val_from, val_to, band, out_w, out_h, out_ll); scene = oracle.line_scene
+LINE_CASES = [
+    ("line_320x240_dark_steady", 320, 240, 352, 1, None, 0.25, 0, 30, None, 160, 120, 320),
+    ("line_640x480_portrait_out", 640, 480, 640, 2, 500, -0.5, 0, 30, None, 240, 320, 480),
+    ("line_640x480_first_band_0_0", 640, 480, 640, 2, 500, -0.5, 0, 30, (0, 0), 320, 240, 640),
+    ("line_320x240_bright_floor", 320, 240, 320, 3, 40, 0.0, 50, 100, None, 200, 150, 401),
+    ("line_64x8_edge_line", 64, 8, 64, 4, 2, 0.0, 0, 30, None, 32, 4, 64),
+    ("line_320x240_empty_range", 320, 240, 320, 5, None, 0.25, 80, 20, None, 160, 120, 320),
+]
+
 
 def main():
     out = {"generator": "tests/golden/make_golden.py", "ranges": RANGES}
@@ -106,6 +117,21 @@ def main():
             "preview_sha256": hashlib.sha256(pv.tobytes()).hexdigest(), "outargs": oa,
         })
     out["runs"] = runs
+    lines = []
+    for name, w, h, ll, seed, x0, slope, vf, vt, band, ow, oh, oll in LINE_CASES:
+        fr = O.line_scene(w, h, ll, seed, x0=x0, slope=slope)
+        rc, oa, pv, sums, band_out = O.line_run(fr, w, h, ll, vf, vt, band=band, out_width=ow,
+                                                out_height=oh, out_line_length=oll)
+        assert rc == 0, name
+        lines.append({
+            "name": name, "width": w, "height": h, "line_length": ll, "seed": seed, "x0": x0,
+            "slope": slope, "val_from": vf, "val_to": vt, "band": list(band) if band else None,
+            "out_width": ow, "out_height": oh, "out_line_length": oll,
+            "frame_sha256": hashlib.sha256(fr.tobytes()).hexdigest(),
+            "preview_sha256": hashlib.sha256(pv.tobytes()).hexdigest(), "outargs": oa,
+            "sums": sums.tolist(), "band_out": list(band_out),
+        })
+    out["line_runs"] = lines
     with open(os.path.join(HERE, "oracle_golden.json"), "w") as f:
         json.dump(out, f, indent=1)
     print("wrote", len(cases), "cases")

@@ -50,15 +50,34 @@ const TRIK_VIDTRANSCODE_CV_Params k_default_params = {{
     {-1, -1},
     1 /* XDM_BYTE */}};
 
-TRIK_VIDTRANSCODE_CV_DynamicParams default_dynamic_params() {  // WGLUE:205-266
+// The algorithms behind a handle: the object sensor (BallDetector, webcam
+// WSEQ and ov7670 OSEQ layouts) or the ov7670 line sensor (LineDetector,
+// LSEQ = trik/ov7670/line_sensor/include/internal/cv_line_detector_seqpass.hpp;
+// its glue trik/ov7670/line_sensor/src/vidtranscode_cv.cpp is WGLUE with
+// YUV422P input and a 240x320 default output).
+enum Algo { kAlgoBall = 0, kAlgoLine = 1 };
+
+const TRIK_VIDTRANSCODE_CV_Params k_default_params_line = {{
+    (int32_t)sizeof(TRIK_VIDTRANSCODE_CV_Params),  // line glue :153-184
+    1,
+    TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_YUV422P,
+    {TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_RGB565X, TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_UNKNOWN},
+    480, 640, 60000, -1,
+    {480, -1},
+    {640, -1},
+    {-1, -1},
+    {-1, -1},
+    1 /* XDM_BYTE */}};
+
+TRIK_VIDTRANSCODE_CV_DynamicParams default_dynamic_params(int algo) {  // WGLUE:205-266
   TRIK_VIDTRANSCODE_CV_DynamicParams d;
   memset(&d, 0, sizeof d);
   d.base.size = (int32_t)sizeof(TRIK_VIDTRANSCODE_CV_DynamicParams);
   d.base.readHeaderOnlyFlag = 0;
   d.base.keepInputResolutionFlag[0] = 0;
   d.base.keepInputResolutionFlag[1] = 1;
-  d.base.outputHeight[0] = 240;
-  d.base.outputWidth[0] = 320;
+  d.base.outputHeight[0] = algo == kAlgoLine ? 320 : 240;  // line glue :214,218 swaps them
+  d.base.outputWidth[0] = algo == kAlgoLine ? 240 : 320;
   d.base.keepInputFrameRateFlag[0] = d.base.keepInputFrameRateFlag[1] = 1;
   d.base.inputFrameRate = -1;
   d.base.outputFrameRate[0] = d.base.outputFrameRate[1] = -1;
@@ -95,6 +114,11 @@ std::string validate_batch(const TrikHsvFrameBatch* b) {
 // ---------------------------------------------------------------------------
 struct TrikCvHandle {
   int device = 0;
+  int algo = kAlgoBall;
+  // line sensor: the cross-point rows the previous run left (LSEQ:298 reads
+  // m_hStart/m_hStop before LSEQ:449-450 sets them); set to the steady state
+  // H/2, H/2+80 by setup (the reference leaves them uninitialised)
+  int32_t line_band[2] = {0, 0};
   TRIK_VIDTRANSCODE_CV_Params params{};
   TRIK_VIDTRANSCODE_CV_DynamicParams dyn{};
   bool alg_ready = false;  // the reference's m_cvAlgorithm is set (WGLUE:302)
@@ -115,7 +139,7 @@ struct TrikCvHandle {
   // preview geometry: scale maps for maps_key = {W, H, out_w, out_h}
   uint32_t* d_maps = nullptr;
   size_t d_maps_cap = 0;
-  int maps_key[4] = {-1, -1, -1, -1};
+  int maps_key[6] = {-1, -1, -1, -1, -1, -1};
   std::vector<uint32_t> h_maps;
 
   // process() staging
@@ -182,9 +206,9 @@ int32_t setup_image_desc(TrikCvHandle* h) {
   const bool out_ok = out_fmt == TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_RGB565X ||
                       (p.numOutputStreams == 0 && out_fmt == TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_UNKNOWN);
   int layout;
-  if (in_fmt == TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_YUV422 && out_ok)
+  if (h->algo == kAlgoBall && in_fmt == TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_YUV422 && out_ok)
     layout = TRIK_HSV_LAYOUT_YUYV;
-  else if (in_fmt == TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_YUV422P && out_ok)
+  else if (in_fmt == TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_YUV422P && out_ok)  // line: YUV422P only
     layout = TRIK_HSV_LAYOUT_OV7670;
   else
     return fail(TRIK_IALG_EFAIL, "cannot create CV algorithm for this format pair");
@@ -196,12 +220,14 @@ int32_t setup_image_desc(TrikCvHandle* h) {
   h->layout = layout;
   h->in_w = in_w; h->in_h = in_h; h->in_ll = in_ll;
   h->out_w = out_w; h->out_h = out_h; h->out_ll = out_ll;
+  h->line_band[0] = in_h / 2;
+  h->line_band[1] = in_h / 2 + 80;
   h->alg_ready = true;
   return TRIK_IALG_EOK;
 }
 
 int32_t setup_dynamic(TrikCvHandle* h, const TRIK_VIDTRANSCODE_CV_DynamicParams* d) {
-  h->dyn = d ? *d : default_dynamic_params();  // WGLUE:271-274
+  h->dyn = d ? *d : default_dynamic_params(h->algo);  // WGLUE:271-274
   return setup_image_desc(h);
 }
 
@@ -281,9 +307,11 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
 inline void set_bit(int32_t& word, int bit) { word |= (int32_t)(1u << bit); }
 
 // Scale maps of the preview (WSEQ:371-387) for this geometry, uploaded once.
-int32_t ensure_maps(TrikCvHandle* h, int w, int hgt, int ow, int oh, hipStream_t s) {
+// col_lo..col_hi: the source columns that write (the line sensor's window).
+int32_t ensure_maps(TrikCvHandle* h, int w, int hgt, int ow, int oh, hipStream_t s, int col_lo = 0,
+                    int col_hi = 0x7FFFFFFF) {
   if (h->d_maps && h->maps_key[0] == w && h->maps_key[1] == hgt && h->maps_key[2] == ow &&
-      h->maps_key[3] == oh)
+      h->maps_key[3] == oh && h->maps_key[4] == col_lo && h->maps_key[5] == col_hi)
     return 0;
   const size_t n = (size_t)w + hgt + ow + oh;
   if (h->tables_busy) HIP_TRY(hipEventSynchronize(h->tables_busy));  // previous users done
@@ -294,10 +322,11 @@ int32_t ensure_maps(TrikCvHandle* h, int w, int hgt, int ow, int oh, hipStream_t
     h->d_maps_cap = n;
   }
   h->h_maps.assign(n ? n : 1, 0u);
-  preview_maps(w, hgt, ow, oh, h->h_maps.data());
+  preview_maps(w, hgt, ow, oh, h->h_maps.data(), col_lo, col_hi);
   HIP_TRY(hipMemcpyAsync(h->d_maps, h->h_maps.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice, s));
   HIP_TRY(hipStreamSynchronize(s));  // h_maps is pageable and reused
   h->maps_key[0] = w; h->maps_key[1] = hgt; h->maps_key[2] = ow; h->maps_key[3] = oh;
+  h->maps_key[4] = col_lo; h->maps_key[5] = col_hi;
   return 0;
 }
 
@@ -324,6 +353,35 @@ PreviewArgs preview_args(const TrikCvHandle* h, const TrikHsvFrameBatch& b,
   return a;
 }
 
+// LSEQ:391-414: hue and saturation bounds fixed at 0..255 (unscaled), value
+// scaled as the object sensor's.
+uint32_t scale_val(int v) {
+  const int s = (v * 255) / 100;
+  return (uint32_t)(s < 0 ? 0 : (s > 255 ? 255 : s));
+}
+PackedRange line_range(int val_from, int val_to) {
+  PackedRange r;
+  r.from = scale_val(val_from) << 16;
+  r.to = (scale_val(val_to) << 16) | 0xFFFFu;
+  r.expect = 0;
+  return r;
+}
+LineArgs line_args(const TrikHsvFrameBatch& b, int val_from, int val_to, int band_start, int band_stop,
+                   TrikHsvTargetSums* sums, TrikHsvTarget* targets) {
+  LineArgs a;
+  a.frames = static_cast<const uint8_t*>(b.frames);
+  a.frame_stride = b.frame_stride;
+  a.n_frames = b.n_frames;
+  a.width = b.width; a.height = b.height; a.line_length = b.line_length;
+  a.val_lo = scale_val(val_from);
+  a.val_hi = scale_val(val_to);
+  a.band_start = band_start;
+  a.band_stop = band_stop;
+  a.sums = sums;
+  a.targets = targets;
+  return a;
+}
+
 AutoRangeArgs auto_range_args(const TrikHsvFrameBatch& b, uint16_t* out) {
   AutoRangeArgs a;
   a.frames = static_cast<const uint8_t*>(b.frames);
@@ -340,8 +398,8 @@ AutoRangeArgs auto_range_args(const TrikHsvFrameBatch& b, uint16_t* out) {
 // ---------------------------------------------------------------------------
 // Layer 1: XDAIS-shaped quartet
 // ---------------------------------------------------------------------------
-extern "C" int32_t TRIK_VIDTRANSCODE_CV_create(const TRIK_VIDTRANSCODE_CV_Params* params,
-                                               TRIK_VIDTRANSCODE_CV_Handle* out_handle) {
+static int32_t create_handle(int algo, const TRIK_VIDTRANSCODE_CV_Params* params,
+                             TRIK_VIDTRANSCODE_CV_Handle* out_handle) {
   if (!out_handle) return fail(TRIK_IALG_EFAIL, "out_handle is NULL");
   *out_handle = nullptr;
   TrikCvHandle* h = new (std::nothrow) TrikCvHandle();
@@ -350,7 +408,8 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_create(const TRIK_VIDTRANSCODE_CV_Params
     delete h;
     return fail(TRIK_IALG_EFAIL, "no HIP device");
   }
-  h->params = params ? *params : k_default_params;  // WGLUE:188-191
+  h->algo = algo;
+  h->params = params ? *params : (algo == kAlgoLine ? k_default_params_line : k_default_params);  // WGLUE:188-191
   const int32_t rc = setup_dynamic(h, nullptr);      // WFXNS:158-163
   if (rc != TRIK_IALG_EOK) {
     release(h);
@@ -358,6 +417,16 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_create(const TRIK_VIDTRANSCODE_CV_Params
   }
   *out_handle = h;
   return TRIK_IALG_EOK;
+}
+
+extern "C" int32_t TRIK_VIDTRANSCODE_CV_create(const TRIK_VIDTRANSCODE_CV_Params* params,
+                                               TRIK_VIDTRANSCODE_CV_Handle* out_handle) {
+  return create_handle(kAlgoBall, params, out_handle);
+}
+
+extern "C" int32_t TRIK_VIDTRANSCODE_CV_create_line(const TRIK_VIDTRANSCODE_CV_Params* params,
+                                                    TRIK_VIDTRANSCODE_CV_Handle* out_handle) {
+  return create_handle(kAlgoLine, params, out_handle);
 }
 
 extern "C" int32_t TRIK_VIDTRANSCODE_CV_delete(TRIK_VIDTRANSCODE_CV_Handle handle) {
@@ -488,6 +557,37 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
         HIP_TRY(hipMemcpyAsync(h->d_frame, in->buf, fb, hipMemcpyHostToDevice, h->stream));
         TrikHsvFrameBatch b = {h->d_frame, (int64_t)fb, 1, h->in_w, h->in_h, h->in_ll, h->layout};
         HIP_TRY(hipMemsetAsync(h->d_sums, 0, sizeof(TrikHsvTargetSums), h->stream));
+        if (h->algo == kAlgoLine) {  // LineDetector::run, LSEQ:376-476
+          const TRIK_VIDTRANSCODE_CV_InArgsAlg& ia = in_args->alg;
+          HIP_TRY(launch_line(line_args(b, ia.detectValFrom, ia.detectValTo, h->line_band[0],
+                                        h->line_band[1], h->d_sums, h->d_targets), h->stream));
+          if (out_ptr && out_size > 0) {  // preview: window columns only, then the overlays
+            const size_t pb = (size_t)out_size;
+            if (pb > h->d_preview_cap) {
+              (void)hipFree(h->d_preview);
+              h->d_preview = nullptr; h->d_preview_cap = 0;
+              HIP_TRY(hipMalloc(&h->d_preview, pb));
+              h->d_preview_cap = pb;
+            }
+            int32_t r = ensure_maps(h, h->in_w, h->in_h, h->out_w, h->out_h, h->stream, 5, h->in_w - 5);
+            if (r) return r;
+            PreviewArgs pa = preview_args(h, b, ia, h->out_w, h->out_h, h->out_ll, h->d_preview, (int64_t)pb);
+            pa.range = line_range(ia.detectValFrom, ia.detectValTo);
+            HIP_TRY(launch_preview_body(pa, h->stream));
+            HIP_TRY(launch_line_overlay(pa, h->d_sums, h->stream));
+            HIP_TRY(hipMemcpyAsync(out_ptr, h->d_preview, pb, hipMemcpyDeviceToHost, h->stream));
+          }
+          TrikHsvTarget t;
+          HIP_TRY(hipMemcpyAsync(&t, h->d_targets, sizeof t, hipMemcpyDeviceToHost, h->stream));
+          HIP_TRY(hipStreamSynchronize(h->stream));
+          oa.targetX = t.x; oa.targetY = t.y; oa.targetSize = t.size;
+          // autoDetectHsv: the line sensor's range detector is a simulated
+          // annealing seeded by srand(time(NULL)) -- not reproducible; detect*
+          // are left untouched.
+          h->line_band[0] = h->in_h / 2;  // LSEQ:449-450, read by the next run
+          h->line_band[1] = h->in_h / 2 + 80;
+          return 0;
+        }
         int32_t r = run_sums(h, &b, &in_args->alg, 1, h->d_sums, nullptr, h->stream);
         if (r) return r;
         HIP_TRY(launch_targets(b, 1, h->d_sums, h->d_targets, h->stream));
@@ -647,6 +747,56 @@ extern "C" int32_t trik_hsv_batch_auto_range(const TrikHsvFrameBatch* b, uint16_
   if (!e.empty()) return fail(TRIK_IVIDTRANSCODE_EFAIL, e);
   if (!out && b->n_frames > 0) return fail(TRIK_IVIDTRANSCODE_EFAIL, "out is NULL");
   HIP_TRY(launch_auto_range(auto_range_args(*b, out), static_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+extern "C" int32_t trik_hsv_line_batch(const TrikHsvFrameBatch* b, int32_t val_from, int32_t val_to,
+                                       int32_t band_start, int32_t band_stop, TrikHsvTargetSums* sums,
+                                       TrikHsvTarget* targets, void* stream) {
+  const std::string e = validate_batch(b);
+  if (!e.empty()) return fail(TRIK_IVIDTRANSCODE_EFAIL, e);
+  if (b->layout != TRIK_HSV_LAYOUT_OV7670)
+    return fail(TRIK_IVIDTRANSCODE_EFAIL, "the line sensor takes the ov7670 layout (YUV422P)");
+  if (b->n_frames > 0 && !sums) return fail(TRIK_IVIDTRANSCODE_EFAIL, "sums is NULL");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (b->n_frames == 0) return 0;
+  HIP_TRY(hipMemsetAsync(sums, 0, sizeof(TrikHsvTargetSums) * (size_t)b->n_frames, s));
+  if (b->width == 0 || b->height == 0) {
+    if (targets) HIP_TRY(hipMemsetAsync(targets, 0, sizeof(TrikHsvTarget) * (size_t)b->n_frames, s));
+    return 0;
+  }
+  HIP_TRY(launch_line(line_args(*b, val_from, val_to, band_start, band_stop, sums, targets), s));
+  return 0;
+}
+
+extern "C" int32_t trik_hsv_line_preview(TRIK_VIDTRANSCODE_CV_Handle h, const TrikHsvFrameBatch* b,
+                                         int32_t val_from, int32_t val_to, const TrikHsvTargetSums* sums,
+                                         int32_t out_width, int32_t out_height, int32_t out_line_length,
+                                         uint8_t* previews, int64_t preview_stride, void* stream) {
+  if (!h) return fail(TRIK_IVIDTRANSCODE_EFAIL, "handle is NULL");
+  const std::string e = validate_batch(b);
+  if (!e.empty()) return fail(TRIK_IVIDTRANSCODE_EFAIL, e);
+  if (b->layout != TRIK_HSV_LAYOUT_OV7670)
+    return fail(TRIK_IVIDTRANSCODE_EFAIL, "the line sensor takes the ov7670 layout (YUV422P)");
+  if (out_width < 0 || out_height < 0 || out_line_length < 2 * out_width)
+    return fail(TRIK_IVIDTRANSCODE_EFAIL, "preview geometry: need out_line_length >= 2*out_width");
+  const int64_t pb = (int64_t)out_height * out_line_length;
+  if (b->n_frames > 1 && preview_stride < pb)
+    return fail(TRIK_IVIDTRANSCODE_EFAIL, "preview_stride smaller than one preview");
+  if (b->n_frames > 0 && pb > 0 && (!previews || !sums)) return fail(TRIK_IVIDTRANSCODE_EFAIL, "NULL buffer");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  std::lock_guard<std::mutex> lock(h->mu);
+  if (b->n_frames == 0 || pb == 0) return 0;
+  int32_t rc = ensure_maps(h, b->width, b->height, out_width, out_height, s, 5, b->width - 5);
+  if (rc) return rc;
+  TRIK_VIDTRANSCODE_CV_InArgsAlg ia;
+  memset(&ia, 0, sizeof ia);
+  PreviewArgs pa = preview_args(h, *b, ia, out_width, out_height, out_line_length, previews, preview_stride);
+  pa.range = line_range(val_from, val_to);
+  HIP_TRY(launch_preview_body(pa, s));
+  HIP_TRY(launch_line_overlay(pa, sums, s));
+  if (!h->tables_busy) HIP_TRY(hipEventCreateWithFlags(&h->tables_busy, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(h->tables_busy, s));
   return 0;
 }
 

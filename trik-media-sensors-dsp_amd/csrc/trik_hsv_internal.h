@@ -100,7 +100,20 @@ struct AutoRangeArgs {
   uint16_t* out;
 };
 
-// Launchers (trik_hsv_kernels.hip, trik_hsv_operator.hip).  Return hipError_t as int.
+// ov7670 line sensor of N frames (trik_hsv_line.hip).  sums[f] = {N, sumX,
+// crossPoints} (crossPoints in the sum_y slot), zeroed by the caller.
+struct LineArgs {
+  const uint8_t* frames;
+  int64_t frame_stride;
+  int32_t n_frames, width, height, line_length;
+  uint32_t val_lo, val_hi;           // scaled V bounds (LSEQ:397-398)
+  int32_t band_start, band_stop;     // cross-point rows (LSEQ:298)
+  TrikHsvTargetSums* sums;
+  TrikHsvTarget* targets;            // may be NULL
+};
+
+// Launchers (trik_hsv_kernels.hip, trik_hsv_operator.hip, trik_hsv_line.hip).
+// Return hipError_t as int.
 int launch_reduce(const KernelArgs& a, bool write_masks, hipStream_t s);
 // The optimised hot kernel (trik_hsv_stripe.hip); returns hipErrorNotSupported
 // when the geometry needs the generic kernel (misaligned input, width > 8192).
@@ -112,11 +125,17 @@ int launch_synth(const TrikHsvFrameBatch& b, uint8_t* frames, int first_frame, i
 // preview_kernel then overlay_kernel (circle from sums[f * sums_pitch])
 int launch_preview(const PreviewArgs& a, const TrikHsvTargetSums* sums, int sums_pitch, hipStream_t s);
 int launch_auto_range(const AutoRangeArgs& a, hipStream_t s);
+int launch_line(const LineArgs& a, hipStream_t s);
+// preview body as launch_preview's first kernel, then the line sensor's overlay
+int launch_preview_body(const PreviewArgs& a, hipStream_t s);
+int launch_line_overlay(const PreviewArgs& a, const TrikHsvTargetSums* sums, hipStream_t s);
 
 // Host side of the preview geometry (trik_hsv_tables.cpp): the reference's
 // scale maps and their inverses, packed as
 //   wi2wo[width], hi2ho[height], last_row[out_h], last_col[out_w]  (32-bit each).
-void preview_maps(int width, int height, int out_w, int out_h, uint32_t* maps);
+// Only source columns col_lo..col_hi write (the line sensor's window).
+void preview_maps(int width, int height, int out_w, int out_h, uint32_t* maps, int col_lo = 0,
+                  int col_hi = 0x7FFFFFFF);
 // Zone bounds of HsvRangeDetector::initImg (hpp:88-108) for zone scale 6.
 void auto_range_zone(int width, int height, int32_t& c_lo, int32_t& c_hi, int32_t& r_lo,
                      int32_t& r_hi);

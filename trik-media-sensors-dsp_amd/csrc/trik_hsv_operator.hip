@@ -266,6 +266,14 @@ __global__ __launch_bounds__(kRangeBlock) void auto_range_kernel(AutoRangeArgs a
 
 }  // namespace
 
+int launch_preview_body(const PreviewArgs& a, hipStream_t s) {
+  if (a.n_frames <= 0 || a.out_w <= 0 || a.out_h <= 0) return hipSuccess;
+  const int64_t blocks = (int64_t)a.n_frames * ((a.out_h + kPreviewRows - 1) / kPreviewRows);
+  if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(preview_kernel, dim3((unsigned)blocks), dim3(64, kPreviewRows), 0, s, a);
+  return hipGetLastError();
+}
+
 int launch_preview(const PreviewArgs& a, const TrikHsvTargetSums* sums, int sums_pitch, hipStream_t s) {
   if (a.n_frames <= 0 || a.out_w <= 0 || a.out_h <= 0) return hipSuccess;
   const int64_t blocks = (int64_t)a.n_frames * ((a.out_h + kPreviewRows - 1) / kPreviewRows);

@@ -80,7 +80,7 @@ void compile_stripe_tables(const RangeTables& base, int n, StripeTables* out) {
   }
 }
 
-void preview_maps(int width, int height, int out_w, int out_h, uint32_t* maps) {
+void preview_maps(int width, int height, int out_w, int out_h, uint32_t* maps, int col_lo, int col_hi) {
   // WSEQ:371-387: shift = min(out/in) in double, maps truncate i * shift
   const double sw = width > 0 ? (double)out_w / width : 0.0;
   const double sh = height > 0 ? (double)out_h / height : 0.0;
@@ -97,7 +97,7 @@ void preview_maps(int width, int height, int out_w, int out_h, uint32_t* maps) {
   for (int i = 0; i < height; ++i)
     if (hi2ho[i] < (uint32_t)out_h) last_row[hi2ho[i]] = i;
   for (int i = 0; i < width; ++i)
-    if (wi2wo[i] < (uint32_t)out_w) last_col[wi2wo[i]] = i;
+    if (i >= col_lo && i <= col_hi && wi2wo[i] < (uint32_t)out_w) last_col[wi2wo[i]] = i;
 }
 
 void auto_range_zone(int width, int height, int32_t& c_lo, int32_t& c_hi, int32_t& r_lo, int32_t& r_hi) {

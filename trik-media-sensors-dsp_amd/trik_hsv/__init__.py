@@ -162,6 +162,46 @@ class Detector:
         return previews
 
 
+    def line_preview(self, frames, width, height, line_length, val_from, val_to, sums, *,
+                     out_width=None, out_height=None, out_line_length=None, n_frames=None,
+                     frame_stride=None, stream=None):
+        """Line-sensor previews (uint8 [N, out_height, out_line_length]) from the
+        per-frame sums of line_batch (LSEQ:283-291, 433-467)."""
+        import torch
+
+        b = _batch(frames, width, height, line_length, LAYOUT_OV7670, n_frames, frame_stride)
+        ow = width // 2 if out_width is None else out_width
+        oh = height // 2 if out_height is None else out_height
+        oll = 2 * ow if out_line_length is None else out_line_length
+        previews = torch.empty((b.n_frames, oh, oll), dtype=torch.uint8, device=frames.device)
+        rc = _lib.trik_hsv_line_preview(self._h, C.byref(b), int(val_from), int(val_to),
+                                        C.c_void_p(sums.data_ptr()), ow, oh, oll,
+                                        C.c_void_p(previews.data_ptr()), oh * oll, _stream_ptr(stream))
+        if rc:
+            raise TrikHsvError(rc, "trik_hsv_line_preview")
+        return previews
+
+
+def line_batch(frames, width, height, line_length, val_from, val_to, *, band=None, n_frames=None,
+               frame_stride=None, stream=None):
+    """The ov7670 line sensor over N frames (LSEQ:376-476): sums int64 [N, 3] =
+    {points, sum_x, cross points} and targets int8 [N, 4] (targetX, targetY =
+    cross size, targetSize).  `band` = the cross-point rows (default: the
+    reference's steady state H/2 .. H/2+80)."""
+    import torch
+
+    b = _batch(frames, width, height, line_length, LAYOUT_OV7670, n_frames, frame_stride)
+    band = (height // 2, height // 2 + 80) if band is None else band
+    sums = torch.empty((b.n_frames, 3), dtype=torch.int64, device=frames.device)
+    targets = torch.empty((b.n_frames, 4), dtype=torch.int8, device=frames.device)
+    rc = _lib.trik_hsv_line_batch(C.byref(b), int(val_from), int(val_to), int(band[0]), int(band[1]),
+                                  C.c_void_p(sums.data_ptr()), C.c_void_p(targets.data_ptr()),
+                                  _stream_ptr(stream))
+    if rc:
+        raise TrikHsvError(rc, "trik_hsv_line_batch")
+    return sums, targets
+
+
 def batch_auto_range(frames, width, height, line_length, layout, *, n_frames=None,
                      frame_stride=None, stream=None):
     """autoDetectHsv per frame: uint16 [N, 6] = hue, hueTol, sat, satTol, val, valTol."""
@@ -238,12 +278,13 @@ def dynamic_params(width, height, line_length, out_width=320, out_height=240, ou
 class ObjectSensor:
     """One TRIK_VIDTRANSCODE_CV codec instance (vidtranscode_cv_fxns.c)."""
 
+    _create = "TRIK_VIDTRANSCODE_CV_create"
+
     def __init__(self, params: _abi.Params | None = None):
         h = C.c_void_p()
-        rc = _lib.TRIK_VIDTRANSCODE_CV_create(C.byref(params) if params is not None else None,
-                                              C.byref(h))
+        rc = getattr(_lib, self._create)(C.byref(params) if params is not None else None, C.byref(h))
         if rc != IALG_EOK:
-            raise TrikHsvError(rc, "TRIK_VIDTRANSCODE_CV_create")
+            raise TrikHsvError(rc, self._create)
         self._h = h
         self.params = params if params is not None else _default_params(1)
 
@@ -297,3 +338,17 @@ class ObjectSensor:
         rc = _lib.TRIK_VIDTRANSCODE_CV_process(self._h, C.byref(ib), C.byref(ob), C.byref(ia),
                                                C.byref(oa))
         return rc, oa
+
+
+class LineSensor(ObjectSensor):
+    """The ov7670 line sensor's codec instance (trik/ov7670/line_sensor glue,
+    LineDetector<YUV422P, RGB565X>): same quartet, YUV422P input; process()
+    uses only detectValFrom/To of the range and ignores autoDetectHsv; OutArgs
+    targetY carries the cross size."""
+
+    _create = "TRIK_VIDTRANSCODE_CV_create_line"
+
+    def __init__(self, params: _abi.Params | None = None):
+        super().__init__(params)
+        if params is None:
+            self.params = _default_params(1, fmt_in=FORMAT_YUV422P)

@@ -141,6 +141,7 @@ class Target(C.Structure):
 # every symbol include/trik_hsv.h declares, with its prototype
 PROTOTYPES = {
     "TRIK_VIDTRANSCODE_CV_create": ([C.POINTER(Params), C.POINTER(C.c_void_p)], i32),
+    "TRIK_VIDTRANSCODE_CV_create_line": ([C.POINTER(Params), C.POINTER(C.c_void_p)], i32),
     "TRIK_VIDTRANSCODE_CV_delete": ([C.c_void_p], i32),
     "TRIK_VIDTRANSCODE_CV_process": ([C.c_void_p, C.POINTER(BufDesc1), C.POINTER(BufDesc),
                                       C.POINTER(InArgs), C.POINTER(OutArgs)], i32),
@@ -159,6 +160,10 @@ PROTOTYPES = {
     "trik_hsv_batch_preview": ([C.c_void_p, C.POINTER(FrameBatch), C.POINTER(InArgsAlg), C.c_void_p,
                                 i32, i32, i32, i32, C.c_void_p, C.c_int64, C.c_void_p], i32),
     "trik_hsv_batch_auto_range": ([C.POINTER(FrameBatch), C.c_void_p, C.c_void_p], i32),
+    "trik_hsv_line_batch": ([C.POINTER(FrameBatch), i32, i32, i32, i32, C.c_void_p, C.c_void_p,
+                             C.c_void_p], i32),
+    "trik_hsv_line_preview": ([C.c_void_p, C.POINTER(FrameBatch), i32, i32, C.c_void_p, i32, i32, i32,
+                               C.c_void_p, C.c_int64, C.c_void_p], i32),
     "trik_hsv_synth": ([C.POINTER(FrameBatch), i32, i32, u64, C.c_void_p], i32),
 }
 
