@@ -33,6 +33,7 @@ GEOMS = [
     (320, 240, 320, 200, 150, 401),
     (320, 240, 384, 160, 120, 320),
     (64, 8, 64, 32, 4, 64),
+    (320, 240, 324, 160, 120, 320),  # lineLength % 8 != 0: the generic kernel
 ]
 SCENES = [(1, None, 0.25, 0, 30), (2, 30, -0.5, 0, 30), (3, 40, 0.0, 50, 100), (4, None, 0.0, 80, 20),
           (5, 2, 0.0, 0, 100)]
@@ -92,13 +93,65 @@ def test_line_batch_many_frames(hsv, oracle_mod):
         assert np.array_equal(pv[i].reshape(-1), ref_pv), i
 
 
+def _exhaustive_ov7670():
+    """A 4096x4096 ov7670 frame holding every (Y, U, V) triple once: pair p
+    (2048 per row) has U = p & 255, V = (p >> 8) & 255, Y = 2k, 2k+1 (k = p >> 16)."""
+    p = np.arange(1 << 23, dtype=np.int64)
+    u, v, k = p & 255, (p >> 8) & 255, p >> 16
+    y = np.stack([2 * k, 2 * k + 1], -1).reshape(4096, 4096).astype(np.uint8)
+    c = np.stack([v, u], -1).reshape(4096, 4096).astype(np.uint8)
+    return np.concatenate([y.reshape(-1), c.reshape(-1)]), y, c
+
+
+def test_line_exhaustive_v_levels(hsv, table):
+    """Every (Y,U,V) triple through the 16-bit V arithmetic: for each percent
+    level p, detections with V range [p, p] (and wide ranges) = the per-pixel
+    table's counts, sums of columns and band counts."""
+    import torch
+
+    fr, y, c = _exhaustive_ov7670()
+    W = H = 4096
+    Y = y.astype(np.int64)
+    V = np.repeat(c[:, 0::2], 2, axis=1).astype(np.int64)
+    U = np.repeat(c[:, 1::2], 2, axis=1).astype(np.int64)
+    val = (table[Y | (U << 8) | (V << 16)] & 0xFFFFFFFF) >> 16
+    cols = np.arange(W)
+    win = (cols >= 5) & (cols <= W - 5)
+    band = (1000, 1700)
+    rows = np.arange(H)
+    in_band = (rows >= band[0]) & (rows <= band[1])
+    dev = torch.from_numpy(fr).cuda()
+    levels = sorted(set(range(0, 101, 1)))
+    ranges = [(p, p) for p in levels] + [(0, 30), (31, 100), (0, 100), (50, 99), (1, 100)]
+    for vf, vt in ranges:
+        lo, hi = (vf * 255) // 100, (vt * 255) // 100
+        det = (val >= lo) & (val <= hi) & win[None, :]
+        ref = [int(det.sum()), int((det * cols[None, :]).sum()), int(det[in_band].sum())]
+        sums, _ = hsv.line_batch(dev, W, H, W, vf, vt, band=band)
+        assert sums[0].cpu().tolist() == ref, (vf, vt)
+
+
+def test_line_wide_frame(hsv, oracle_mod):
+    """W > 8192 (column chunks), H = 8 (one row segment)."""
+    import torch
+
+    w, h, ll = 8448, 8, 8448
+    fr = oracle_mod.line_scene(w, h, ll, 77, x0=6000, slope=1.0, line_w=300)
+    dev = torch.from_numpy(fr).cuda()
+    for band in (None, (2, 5)):
+        sums, targets = hsv.line_batch(dev, w, h, ll, 0, 30, band=band)
+        _, oa, _, ref, _ = oracle_mod.line_run(fr, w, h, ll, 0, 30, band=band, preview=False)
+        assert sums[0].cpu().tolist() == ref.tolist()
+        assert tuple(targets[0, :3].cpu().tolist()) == _targets(oa)
+
+
 def _line_sensor(hsv, w, h, ll, ow, oh, oll):
     s = hsv.LineSensor(hsv._default_params(1, hsv.FORMAT_YUV422P, max(640, w, ow), max(480, h, oh)))
     assert s.set_params(w, h, ll, out_width=ow, out_height=oh, out_line_length=oll) == 0
     return s
 
 
-@pytest.mark.parametrize("geom", GEOMS[:4])
+@pytest.mark.parametrize("geom", GEOMS[:4] + GEOMS[5:])
 def test_line_sensor_process_vs_oracle(hsv, oracle_mod, geom):
     """process() frame after frame: OutArgs + preview, the cross band carried
     from run to run (LSEQ:298-299, 449-450); detect* untouched (autoDetectHsv
