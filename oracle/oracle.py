@@ -42,6 +42,17 @@ class Range(C.Structure):
     ]
 
 
+class BlobArgs(C.Structure):
+    """trik_oracle_blob_args: ov7670 object sensor InArgsAlg (ov7670 trik_vidtranscode_cv.h:44-53)."""
+    _fields_ = [("set_hsv_range", C.c_int32), ("hue", C.c_uint16), ("hue_tol", C.c_uint16),
+                ("sat", C.c_uint8), ("sat_tol", C.c_uint8), ("val", C.c_uint8), ("val_tol", C.c_uint8),
+                ("auto_detect", C.c_int32)]
+
+
+class BlobState(C.Structure):
+    _fields_ = [("from_", C.c_uint32), ("to", C.c_uint32), ("expect", C.c_uint32)]
+
+
 def build() -> str:
     """Compile liboracle.so in place (gcc) and return its path."""
     subprocess.run(["make", "-s", "-C", HERE], check=True)
@@ -99,6 +110,12 @@ def lib():
                                            vp, C.c_int, C.c_int, C.c_int, vp, i64,
                                            C.POINTER(OutArgs), vp]
         L.trik_oracle_line_run.restype = C.c_int
+        L.trik_oracle_blob_range.argtypes = [C.POINTER(BlobArgs), C.POINTER(BlobState)]
+        L.trik_oracle_blob_range.restype = None
+        L.trik_oracle_blob_run.argtypes = [vp, i64, C.c_int, C.c_int, C.c_int, C.POINTER(BlobArgs),
+                                           C.POINTER(BlobState), C.c_int, C.c_int, C.c_int, vp, i64,
+                                           vp, vp, vp, vp, vp]
+        L.trik_oracle_blob_run.restype = C.c_int
         _lib = L
     return _lib
 
@@ -247,4 +264,106 @@ def line_scene(width, height, line_length, seed, x0=None, slope=0.25, line_w=24)
         lo, hi = max(0, a), min(width, a + line_w)
         if lo < hi:
             y[r, lo:hi] = rng.integers(10, 50, hi - lo)
+    return fr
+
+
+def blob_range(hsv):
+    """(hue, hueTol, sat, satTol, val, valTol) -> packed (from, to, expect), BMB:110-130."""
+    st = BlobState()
+    lib().trik_oracle_blob_range(C.byref(BlobArgs(1, *[int(v) for v in hsv], 0)), C.byref(st))
+    return st.from_, st.to, st.expect
+
+
+def blob_run(frame_u8: np.ndarray, width, height, line_length, hsv=None, state=None, out_width=None,
+             out_height=None, out_line_length=None, preview=True):
+    """The ov7670 object sensor's run (OSEQ:516-602: bitmap + clusterer -> 8 targets).
+
+    hsv: (hue, hueTol, sat, satTol, val, valTol) with setHsvRange, or None to keep
+    `state` (the sticky packed range; default all-zero).  Returns a dict with rc,
+    targets int8 [8,3] (x, y, size), preview, meta uint8 [H/4, W/4], labels uint16,
+    top int32 [8,3] (size, sum_x, sum_y), n_labels and state (from, to, expect)."""
+    fr = np.ascontiguousarray(frame_u8, dtype=np.uint8)
+    ow = width // 2 if out_width is None else out_width
+    oh = height // 2 if out_height is None else out_height
+    oll = 2 * ow if out_line_length is None else out_line_length
+    out = np.zeros(max(1, oh * oll), np.uint8) if preview else None
+    st = BlobState(*(state if state is not None else (0, 0, 0)))
+    a = BlobArgs(1 if hsv is not None else 0, *([int(v) for v in hsv] if hsv is not None else [0] * 6), 0)
+    bw, bh = max(width // 4, 0), max(height // 4, 0)
+    targets = np.zeros(24, np.int8)
+    meta = np.zeros(max(1, bw * bh), np.uint8)
+    labels = np.zeros(max(1, bw * bh), np.uint16)
+    top = np.zeros(24, np.int32)
+    n = C.c_int32(0)
+    rc = lib().trik_oracle_blob_run(_ptr(fr), fr.size, width, height, line_length, C.byref(a),
+                                    C.byref(st), ow, oh, oll, _ptr(out) if out is not None else None,
+                                    out.size if out is not None else 0, _ptr(targets), _ptr(meta),
+                                    _ptr(labels), _ptr(top), C.byref(n))
+    return {"rc": rc, "targets": targets.reshape(8, 3), "preview": out[:oh * oll] if out is not None else None,
+            "meta": meta[:bw * bh].reshape(bh, bw), "labels": labels[:bw * bh].reshape(bh, bw),
+            "top": top.reshape(8, 3), "n_labels": n.value, "state": (st.from_, st.to, st.expect)}
+
+
+def blob_scene(width, height, line_length, seed, blobs=((0.3, 0.4, 0.12), (0.7, 0.6, 0.08)),
+               noise=0.0) -> np.ndarray:
+    """A test ov7670 frame for the multi-blob sensor: grey textured floor with
+    red discs (centre x, centre y as fractions, radius as a fraction of H) and
+    optional salt of red pixels (fraction `noise`); random padding bytes."""
+    rng = np.random.default_rng(seed)
+    fr = rng.integers(0, 256, 2 * height * line_length, dtype=np.uint8)
+    y = fr[: height * line_length].reshape(height, line_length)
+    c = fr[height * line_length:].reshape(height, line_length)
+    y[:, :width] = rng.integers(90, 170, (height, width))
+    c[:, :width] = rng.integers(118, 138, (height, width))
+    yy, xx = np.mgrid[0:height, 0:width]
+    red = np.zeros((height, width), bool)
+    for cx, cy, r in blobs:
+        red |= (xx - cx * width) ** 2 + (yy - cy * height) ** 2 <= (r * height) ** 2
+    if noise:
+        red |= rng.random((height, width)) < noise
+    y[:, :width][red] = rng.integers(70, 90, int(red.sum()))
+    ch = c[:, :width]
+    # red: V (even chroma byte) high, U (odd) low -- per pair, so mark a pair if either pixel is red
+    pair_red = red[:, 0::2] | red[:, 1::2]
+    v = ch[:, 0::2]
+    u = ch[:, 1::2]
+    v[pair_red] = rng.integers(200, 230, int(pair_red.sum()))
+    u[pair_red] = rng.integers(90, 110, int(pair_red.sum()))
+    ch[:, 0::2], ch[:, 1::2] = v, u
+    return fr
+
+
+RED_HSV = (0, 20, 80, 20, 50, 50)  # a range the red of blob_scene / blob_frame falls in
+
+
+def blob_frame(meta: np.ndarray, line_length=None, seed=0) -> np.ndarray:
+    """An ov7670 frame whose set metapixels (meta [bh, bw], nonzero = set) are
+    red 4x4 blocks with 3..16 red pixels and the rest grey (so under RED_HSV
+    exactly the given metapixels are set); the grey blocks get 0..2 red pixels."""
+    rng = np.random.default_rng(seed)
+    bh, bw = meta.shape
+    h, w = 4 * bh, 4 * bw
+    ll = w if line_length is None else line_length
+    fr = rng.integers(0, 256, 2 * h * ll, dtype=np.uint8)
+    y = fr[: h * ll].reshape(h, ll)
+    c = fr[h * ll:].reshape(h, ll)
+    # red pixel counts per block: set -> 3..16, clear -> 0..2; red pixels come in
+    # chroma pairs, so counts are realised on pairs (2 px) plus single-pixel Y changes
+    red = np.zeros((h, w), bool)
+    for (r, q), m in np.ndenumerate(meta):
+        k = int(rng.integers(3, 17)) if m else int(rng.integers(0, 3))
+        idx = rng.permutation(16)[:k]
+        red[4 * r + idx // 4, 4 * q + idx % 4] = True
+    # a pixel is red iff its pair carries red chroma AND its Y is the dark value;
+    # grey pixels of a red pair get a bright Y that falls outside RED_HSV
+    pair = red[:, 0::2] | red[:, 1::2]
+    y[:, :w] = np.where(red, 80, 0).astype(np.uint8)
+    c[:, :w] = 128
+    cv = c[:, :w]
+    cv[:, 0::2] = np.where(pair, 215, 128)
+    cv[:, 1::2] = np.where(pair, 100, 128)
+    yv = y[:, :w]
+    grey_in_red_pair = ~red & np.repeat(pair, 2, axis=1)
+    yv[grey_in_red_pair] = 250
+    yv[~red & ~grey_in_red_pair] = rng.integers(100, 160, int((~red & ~grey_in_red_pair).sum()))
     return fr

@@ -788,3 +788,204 @@ int trik_oracle_line_run(const uint8_t* frame, int64_t frame_size, int width, in
   free(hi2ho);
   return 0;
 }
+
+/* ------------------------------------------------------------------------ */
+/* ov7670 object sensor: metapixel bitmap + clusterer (OSEQ:516-602).        */
+/* ------------------------------------------------------------------------ */
+
+static int value_range(int v, int adj, int lo, int hi) { /* makeValueRange, stdcpp.hpp:70-79 */
+  v += adj;
+  return v > hi ? hi : (v < lo ? lo : v);
+}
+static int value_wrap(int v, int adj, int lo, int hi) { /* makeValueWrap, stdcpp.hpp:81-90 */
+  v += adj;
+  while (v > hi) v -= hi - lo + 1;
+  while (v < lo) v += hi - lo + 1;
+  return v;
+}
+
+void trik_oracle_blob_range(const trik_oracle_blob_args* a, trik_oracle_blob_state* st) {
+  /* BMB:110-130: from/to around the centre, scaled as the webcam's (int16 range) */
+  const int hf = value_wrap(a->hue, -(int)a->hue_tol, 0, 359);
+  const int ht = value_wrap(a->hue, +(int)a->hue_tol, 0, 359);
+  const int sf = value_range(a->sat, -(int)a->sat_tol, 0, 100);
+  const int st_ = value_range(a->sat, +(int)a->sat_tol, 0, 100);
+  const int vf = value_range(a->val, -(int)a->val_tol, 0, 100);
+  const int vt = value_range(a->val, +(int)a->val_tol, 0, 100);
+  const uint32_t h0 = (uint32_t)clamp_range(0, (hf * 255) / 359, 255);
+  const uint32_t h1 = (uint32_t)clamp_range(0, (ht * 255) / 359, 255);
+  const uint32_t s0 = (uint32_t)clamp_range(0, (sf * 255) / 100, 255);
+  const uint32_t s1 = (uint32_t)clamp_range(0, (st_ * 255) / 100, 255);
+  const uint32_t v0 = (uint32_t)clamp_range(0, (vf * 255) / 100, 255);
+  const uint32_t v1 = (uint32_t)clamp_range(0, (vt * 255) / 100, 255);
+  if (h0 <= h1) { /* resetHsvRange, BMB:62-77 */
+    st->from = (v0 << 16) | (s0 << 8) | h0;
+    st->to = (v1 << 16) | (s1 << 8) | h1;
+    st->expect = 0;
+  } else {
+    st->from = (v0 << 16) | (s0 << 8) | ((h1 + 1) & 0xFFu);
+    st->to = (v1 << 16) | (s1 << 8) | ((h0 - 1) & 0xFFu);
+    st->expect = 1;
+  }
+}
+
+static int blob_pop16(uint16_t x) { /* pop(), stdcpp.hpp:58-68 */
+  int n = 0;
+  for (; x; x &= (uint16_t)(x - 1)) ++n;
+  return n;
+}
+
+/* CLU:44-52: the smallest non-zero of the four, 0 when all are 0 */
+static uint16_t blob_min4(const uint16_t a[4]) {
+  uint16_t v = a[0];
+  for (int n = 1; n < 4; ++n)
+    if ((a[n] < v && a[n] != 0) || v == 0) v = a[n];
+  return v;
+}
+
+typedef struct blob_cluster { int32_t x, y, size, label; } blob_cluster;
+
+/* size descending, ties by ascending label: an insertion-stable merge sort */
+static void blob_sort(blob_cluster* c, blob_cluster* tmp, int n) {
+  for (int w = 1; w < n; w *= 2)
+    for (int lo = 0; lo < n; lo += 2 * w) {
+      const int mid = lo + w < n ? lo + w : n, hi = lo + 2 * w < n ? lo + 2 * w : n;
+      int i = lo, j = mid, k = lo;
+      while (i < mid && j < hi) tmp[k++] = (c[j].size > c[i].size) ? c[j++] : c[i++];
+      while (i < mid) tmp[k++] = c[i++];
+      while (j < hi) tmp[k++] = c[j++];
+      for (k = lo; k < hi; ++k) c[k] = tmp[k];
+    }
+}
+
+int trik_oracle_blob_run(const uint8_t* frame, int64_t frame_size, int width, int height,
+                         int line_length, const trik_oracle_blob_args* args,
+                         trik_oracle_blob_state* state, int out_width, int out_height,
+                         int out_line_length, uint8_t* out, int64_t out_size, int8_t targets[24],
+                         uint8_t* meta, uint16_t* labels_out, int32_t top[24], int32_t* n_labels) {
+  memset(targets, 0, 24);
+  if (top) memset(top, 0, 24 * sizeof(int32_t));
+  if (n_labels) *n_labels = 0;
+  if (width < 0 || height < 0 || width % 32 != 0 || height % 4 != 0) return -1; /* OSEQ:462-466 */
+  if (2LL * height * line_length > frame_size) return -1; /* both planes (OSEQ:517, :347) */
+  if (out && (int64_t)out_height * out_line_length > out_size) return -1;
+  const int bw = width / 4, bh = height / 4; /* OSEQ:441-444 */
+  if ((int64_t)((bw + 1) / 2) * ((bh + 1) / 2) + 1 > 65535) return -1; /* uint16 labels */
+  if (args->set_hsv_range) trik_oracle_blob_range(args, state);
+
+  const double sw = (double)out_width / width, sh = (double)out_height / height;
+  const double shift = sw < sh ? sw : sh; /* OSEQ:468-470 */
+  const size_t npx = (size_t)((int64_t)width * height > 0 ? (int64_t)width * height : 1);
+  const size_t nmp = (size_t)(bw * bh > 0 ? bw * bh : 1);
+  uint32_t* wi2wo = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(width > 0 ? width : 1));
+  uint32_t* hi2ho = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(height > 0 ? height : 1));
+  uint32_t* rgb = (uint32_t*)malloc(sizeof(uint32_t) * npx);
+  uint16_t* bitmap = (uint16_t*)calloc(nmp, sizeof(uint16_t));
+  uint16_t* lab = (uint16_t*)calloc(nmp, sizeof(uint16_t));
+  uint16_t* eq = (uint16_t*)malloc(sizeof(uint16_t) * (nmp + 2));
+  blob_cluster* cl = (blob_cluster*)malloc(sizeof(blob_cluster) * (nmp + 2));
+  blob_cluster* tmp = (blob_cluster*)malloc(sizeof(blob_cluster) * (nmp + 2));
+  if (!wi2wo || !hi2ho || !rgb || !bitmap || !lab || !eq || !cl || !tmp) {
+    free(wi2wo); free(hi2ho); free(rgb); free(bitmap); free(lab); free(eq); free(cl); free(tmp);
+    return -1;
+  }
+  for (int i = 0; i < width; ++i) wi2wo[i] = (uint32_t)(i * shift);
+  for (int i = 0; i < height; ++i) hi2ho[i] = (uint32_t)(i * shift);
+
+  int n = 1; /* CLU:180-183: label 0 is the background */
+  eq[0] = 0;
+  memset(&cl[0], 0, sizeof cl[0]);
+  if (height > 0 && width > 0) {
+    for (int row = 0; row < height; ++row) /* convertImageYuyvToHsv + BitmapBuilder::run */
+      for (int q = 0; q < width / 2; ++q) {
+        uint32_t px[2];
+        trik_oracle_pair_rgb_c64x(pair_word(frame, height, line_length, TRIK_ORACLE_LAYOUT_OV7670, row, q), px);
+        for (int k = 0; k < 2; ++k) {
+          const int col = 2 * q + k;
+          rgb[(int64_t)row * width + col] = px[k];
+          const int det = trik_oracle_detect(trik_oracle_hsv_c64x(px[k]), state->from, state->to, state->expect);
+          bitmap[(row / 4) * bw + col / 4] |= (uint16_t)(det << ((row % 4) * 4 + col % 4));
+        }
+      }
+    for (int r = 0; r < bh; ++r) /* Clusterizer::run, CLU:185-190 */
+      for (int c = 0; c < bw; ++c) {
+        if (blob_pop16(bitmap[r * bw + c]) <= 2) continue;
+        uint16_t a[4] = {0, 0, 0, 0}; /* left, up-left, up, up-right (CLU:70-84) */
+        if (r != 0) {
+          a[2] = lab[(r - 1) * bw + c];
+          if (c != 0) a[1] = lab[(r - 1) * bw + c - 1];
+          if (c != bw - 1) a[3] = lab[(r - 1) * bw + c + 1];
+        }
+        if (c != 0) a[0] = lab[r * bw + c - 1];
+        const uint16_t m = blob_min4(a);
+        if (m) { /* CLU:91-97 */
+          lab[r * bw + c] = m;
+          cl[m].x += c;
+          cl[m].y += r;
+          cl[m].size++;
+          for (int i = 0; i < 4; ++i)
+            if (a[i] && !(a[i] == m || eq[a[i]] == eq[m])) eq[a[i]] = eq[m];
+        } else { /* CLU:98-112: new label, its first metapixel not counted */
+          lab[r * bw + c] = (uint16_t)n;
+          eq[n] = (uint16_t)n;
+          memset(&cl[n], 0, sizeof cl[n]);
+          ++n;
+        }
+      }
+  }
+  for (int i = 0; i < n; ++i) { /* postProcessing, CLU:115-127 */
+    cl[i].label = i;
+    if (i != eq[i]) {
+      cl[eq[i]].x += cl[i].x;
+      cl[eq[i]].y += cl[i].y;
+      cl[eq[i]].size += cl[i].size;
+      cl[i].size = 0;
+    }
+  }
+  blob_sort(cl, tmp, n);
+  if (n_labels) *n_labels = n;
+  if (meta)
+    for (int i = 0; i < bw * bh; ++i) meta[i] = blob_pop16(bitmap[i]) > 2;
+  if (labels_out) memcpy(labels_out, lab, sizeof(uint16_t) * (size_t)(bw * bh));
+
+  const run_ctx ctx = {width, height, out_line_length, wi2wo, hi2ho, out};
+  if (out && width > 0 && height > 0) {
+    for (int row = 0; row < height; ++row) /* proceedImageHsv, OSEQ:387-420 */
+      for (int col = 0; col < width; ++col) {
+        const int det = lab[(row / 4) * bw + col / 4] != 0; /* getMinEqCluster(label) != 0 */
+        write_px(out + (int64_t)hi2ho[row] * out_line_length + (int64_t)wi2wo[col] * 2,
+                 det ? 0x00ffffu : rgb[(int64_t)row * width + col]);
+      }
+    const int step = height / 6, h_height = height / 2, h_width = width / 2; /* OSEQ:548-561 */
+    draw_vline(&ctx, h_width - step, h_height, 0xff00ff);
+    draw_vline(&ctx, h_width + step, h_height, 0xff00ff);
+    draw_vline(&ctx, h_width - 2 * step, h_height, 0xff00ff);
+    draw_vline(&ctx, h_width + 2 * step, h_height, 0xff00ff);
+    draw_hline(&ctx, h_width, h_height - step, 0xff00ff);
+    draw_hline(&ctx, h_width, h_height + step, 0xff00ff);
+    draw_hline(&ctx, h_width, h_height - 2 * step, 0xff00ff);
+    draw_hline(&ctx, h_width, h_height + 2 * step, 0xff00ff);
+  }
+  for (int i = 0; i < 8; ++i) { /* OSEQ:563-590 */
+    const int32_t csize = i < n ? cl[i].size : 0;
+    if (top && i < n) {
+      top[3 * i] = cl[i].size;
+      top[3 * i + 1] = cl[i].x;
+      top[3 * i + 2] = cl[i].y;
+    }
+    const int root = (int)sqrtf((float)(uint16_t)csize); /* getSize() is uint16_t */
+    const uint32_t radius = (uint32_t)ceilf((float)root / 3.1415927f);
+    const int size = (int)((radius * 100u * 4u) / (uint32_t)(bw + bh));
+    if (size > 4) {
+      const int32_t x = (cl[i].x / (csize + 1)) * 4, y = (cl[i].y / (csize + 1)) * 4; /* CLU:139-147 */
+      if (out && width > 0 && height > 0)
+        for (int dc = -1; dc <= 1; ++dc) /* drawFatPixel, OSEQ:92-108 */
+          for (int dr = -1; dr <= 1; ++dr) draw_bound(&ctx, x + dc, y + dr, 0xff0000);
+      targets[3 * i + 2] = (int8_t)(uint8_t)size;
+      targets[3 * i] = (int8_t)(((x - width / 2) * 100 * 2) / width);
+      targets[3 * i + 1] = (int8_t)(((y - height / 2) * 100 * 2) / height);
+    }
+  }
+  free(wi2wo); free(hi2ho); free(rgb); free(bitmap); free(lab); free(eq); free(cl); free(tmp);
+  return 0;
+}

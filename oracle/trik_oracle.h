@@ -167,6 +167,64 @@ int      trik_oracle_line_run(const uint8_t* frame, int64_t frame_size, int widt
                               int out_width, int out_height, int out_line_length, uint8_t* out,
                               int64_t out_size, trik_oracle_outargs* oa, int64_t sums[3]);
 
+/* ---- ov7670 object sensor: metapixel bitmap + clusterer -> 8 targets ------
+ * BLOB = BallDetector<YUV422P, RGB565X> of trik/ov7670/object_sensor/include/
+ * internal/cv_ball_detector_seqpass.hpp:516-602 (OSEQ), with BitmapBuilder
+ * (cv_bitmap_builder_reference.hpp:107-217, BMB) and Clusterizer
+ * (cv_clusterizer_reference.hpp:85-202, CLU). */
+
+/* TRIK_VIDTRANSCODE_CV_InArgsAlg of trik/ov7670/object_sensor/
+ * trik_vidtranscode_cv.h:44-53 (XDAS_Bool restated as int32). */
+typedef struct trik_oracle_blob_args {
+  int32_t set_hsv_range;
+  uint16_t hue, hue_tol;    /* 0..359 */
+  uint8_t sat, sat_tol;     /* 0..100 */
+  uint8_t val, val_tol;     /* 0..100 */
+  int32_t auto_detect;      /* not restated (srand(time) annealing) */
+} trik_oracle_blob_args;
+
+/* BitmapBuilder's sticky packed range (BMB:45-46, 62-77): set only when
+ * set_hsv_range; uninitialised in the reference before that, zero here. */
+typedef struct trik_oracle_blob_state {
+  uint32_t from, to, expect;
+} trik_oracle_blob_state;
+
+/* BMB:110-130 + resetHsvRange: centre/tolerance -> packed range */
+void     trik_oracle_blob_range(const trik_oracle_blob_args* a, trik_oracle_blob_state* st);
+
+/* One run:
+ *   - per-pixel HSV (the object sensor's, ov7670 planes) and detection with the
+ *     sticky range (updated first when set_hsv_range);
+ *   - bitmap: 4x4 metapixels of bw = W/4 x bh = H/4, bit (row%4)*4 + col%4
+ *     (BMB:171-190); a metapixel is "set" when more than 2 of its 16 pixels
+ *     are detected (CLU:185-186);
+ *   - clusterer, literally: raster scan over set metapixels, label = the
+ *     smallest non-zero label among left, up-left, up, up-right (CLU:70-84,
+ *     44-52), else a new label whose first metapixel is not counted
+ *     (CLU:98-112); equivalences one level deep (CLU:92-96); postProcessing
+ *     folds each label into its equivalence target in label order, zeroing
+ *     only the size (CLU:115-127);
+ *   - sort by size, descending; ties by ascending label (the reference's
+ *     std::sort leaves their order unspecified);
+ *   - targets i < 8 (OSEQ:572-598): r = ceil(floor(sqrt(size)) / pi),
+ *     size% = r*400/(bw+bh), kept when > 4, x/y = (sum / (size+1)) * 4 in
+ *     percent of the half-frame; entries past the label count have size 0
+ *     (the reference reads past the end of its vector);
+ *   - preview: every pixel through the truncated double scale maps, set
+ *     metapixels as 0x00ffff (OSEQ:387-420), the 8 guide lines, then a 3x3
+ *     red "fat pixel" per kept target (OSEQ:556-580).
+ * targets: 8 x {x, y, size}; meta (optional, bw*bh): 1 for set metapixels;
+ * labels (optional, bw*bh): the label map; top (optional, 8 x {size, sum_x,
+ * sum_y} after postProcessing and sorting); *n_labels: labels including 0.
+ * Returns -1 where setup/run would fail, or when the label count could
+ * exceed the reference's uint16 labels. */
+int      trik_oracle_blob_run(const uint8_t* frame, int64_t frame_size, int width, int height,
+                              int line_length, const trik_oracle_blob_args* args,
+                              trik_oracle_blob_state* state, int out_width, int out_height,
+                              int out_line_length, uint8_t* out, int64_t out_size,
+                              int8_t targets[24], uint8_t* meta, uint16_t* labels,
+                              int32_t top[24], int32_t* n_labels);
+
 #ifdef __cplusplus
 }
 #endif

@@ -78,6 +78,17 @@ LINE_CASES = [
     ("line_320x240_empty_range", 320, 240, 320, 5, None, 0.25, 80, 20, None, 160, 120, 320),
 ]
 
+# ov7670 multi-blob sensor (OSEQ:516-602): scenes (oracle.blob_scene) and
+# bitmap-driven frames (oracle.blob_frame of a random metapixel map)
+BLOB_CASES = [
+    ("blob_320x240_two_discs", "scene", 320, 240, 320, 1, 0.0, None, (0, 20, 80, 20, 50, 50), 160, 120, 320),
+    ("blob_640x480_discs_salt", "scene", 640, 480, 704, 2, 0.01, None, (0, 20, 80, 20, 50, 50), 320, 240, 640),
+    ("blob_160x120_meta_half", "meta", 160, 120, 176, 3, None, 0.5, (0, 20, 80, 20, 50, 50), 80, 60, 160),
+    ("blob_160x120_meta_sparse", "meta", 160, 120, 160, 4, None, 0.12, (0, 20, 80, 20, 50, 50), 96, 72, 200),
+    ("blob_320x240_meta_dense", "meta", 320, 240, 320, 5, None, 0.8, (0, 20, 80, 20, 50, 50), 160, 120, 320),
+    ("blob_320x240_no_match", "scene", 320, 240, 320, 6, 0.0, None, (180, 10, 50, 10, 50, 10), 160, 120, 320),
+]
+
 
 def main():
     out = {"generator": "tests/golden/make_golden.py", "ranges": RANGES}
@@ -132,6 +143,25 @@ def main():
             "sums": sums.tolist(), "band_out": list(band_out),
         })
     out["line_runs"] = lines
+    blobs = []
+    for name, kind, w, h, ll, seed, noise, dens, hsv, ow, oh, oll in BLOB_CASES:
+        if kind == "scene":
+            fr = O.blob_scene(w, h, ll, seed, noise=noise)
+        else:
+            rng = np.random.default_rng(seed)
+            meta = (rng.random((h // 4, w // 4)) < dens).astype(np.uint8)
+            fr = O.blob_frame(meta, ll, seed=seed)
+        r = O.blob_run(fr, w, h, ll, hsv=hsv, out_width=ow, out_height=oh, out_line_length=oll)
+        assert r["rc"] == 0, name
+        blobs.append({
+            "name": name, "kind": kind, "width": w, "height": h, "line_length": ll, "seed": seed,
+            "noise": noise, "density": dens, "hsv": list(hsv), "out_width": ow, "out_height": oh,
+            "out_line_length": oll, "frame_sha256": hashlib.sha256(fr.tobytes()).hexdigest(),
+            "targets": r["targets"].tolist(), "top": r["top"].tolist(), "n_labels": r["n_labels"],
+            "preview_sha256": hashlib.sha256(r["preview"].tobytes()).hexdigest(),
+            "labels_sha256": hashlib.sha256(r["labels"].tobytes()).hexdigest(),
+        })
+    out["blob_runs"] = blobs
     with open(os.path.join(HERE, "oracle_golden.json"), "w") as f:
         json.dump(out, f, indent=1)
     print("wrote", len(cases), "cases")
