@@ -165,6 +165,43 @@ typedef struct TRIK_VIDTRANSCODE_CV_OutArgsAlg {
   uint16_t detectValTolerance;
 } TRIK_VIDTRANSCODE_CV_OutArgsAlg;
 
+/* The ov7670 object sensor's InArgsAlg (OPUB:51-60): a centre and tolerance
+ * per channel, applied when setHsvRange is set and kept until the next set
+ * (BitmapBuilder, cv_bitmap_builder_reference.hpp:110-130). */
+typedef struct TRIK_VIDTRANSCODE_CV_OV7670_InArgsAlg {
+  int32_t setHsvRange;
+  uint16_t detectHue;    /* [0..359] */
+  uint16_t detectHueTol; /* [0..359] */
+  uint8_t detectSat;     /* [0..100] */
+  uint8_t detectSatTol;
+  uint8_t detectVal;     /* [0..100] */
+  uint8_t detectValTol;
+  int32_t autoDetectHsv; /* not reproduced (srand(time) annealing); detect* untouched */
+} TRIK_VIDTRANSCODE_CV_OV7670_InArgsAlg;
+
+typedef struct TRIK_VIDTRANSCODE_CV_OV7670_InArgs { /* OPUB:62-65 */
+  TRIK_IVIDTRANSCODE_InArgs base;
+  TRIK_VIDTRANSCODE_CV_OV7670_InArgsAlg alg;
+} TRIK_VIDTRANSCODE_CV_OV7670_InArgs;
+
+/* XDAS_Target, OPUB:67-71 */
+typedef struct TRIK_XDAS_Target {
+  int8_t x;     /* [-100..100] */
+  int8_t y;     /* [-100..100] */
+  uint8_t size; /* [0..100] */
+} TRIK_XDAS_Target;
+
+/* The ov7670 object sensor's OutArgsAlg, OPUB:73-81 */
+typedef struct TRIK_VIDTRANSCODE_CV_OV7670_OutArgsAlg {
+  TRIK_XDAS_Target target[8];
+  uint16_t detectHue;
+  uint16_t detectHueTolerance;
+  uint16_t detectSat;
+  uint16_t detectSatTolerance;
+  uint16_t detectVal;
+  uint16_t detectValTolerance;
+} TRIK_VIDTRANSCODE_CV_OV7670_OutArgsAlg;
+
 /* XDM1_SingleBufDesc */
 typedef struct TRIK_XDM1_SingleBufDesc {
   int8_t* buf;
@@ -208,6 +245,11 @@ typedef struct TRIK_VIDTRANSCODE_CV_OutArgs { /* WPUB:76-79 */
   TRIK_VIDTRANSCODE_CV_OutArgsAlg alg;
 } TRIK_VIDTRANSCODE_CV_OutArgs;
 
+typedef struct TRIK_VIDTRANSCODE_CV_OV7670_OutArgs { /* OPUB:83-86 */
+  TRIK_IVIDTRANSCODE_OutArgs base;
+  TRIK_VIDTRANSCODE_CV_OV7670_OutArgsAlg alg;
+} TRIK_VIDTRANSCODE_CV_OV7670_OutArgs;
+
 /* XDM1_AlgBufInfo subset filled by GETSTATUS/GETBUFINFO (WFXNS:287-297) */
 typedef struct TRIK_XDM1_AlgBufInfo {
   int32_t minNumInBufs;
@@ -250,6 +292,18 @@ int32_t TRIK_VIDTRANSCODE_CV_create(const TRIK_VIDTRANSCODE_CV_Params* params,
  * seeded by srand(time(NULL))). */
 int32_t TRIK_VIDTRANSCODE_CV_create_line(const TRIK_VIDTRANSCODE_CV_Params* params,
                                          TRIK_VIDTRANSCODE_CV_Handle* out_handle);
+
+/* The quartet for the ov7670 object sensor's codec (trik/ov7670/object_sensor:
+ * BallDetector<YUV422P, RGB565X> of include/internal/
+ * cv_ball_detector_seqpass.hpp:516-602 -- OSEQ -- with its BitmapBuilder and
+ * Clusterizer).  params == NULL takes that glue's defaults (YUV422P in,
+ * RGB565X out).  process() then takes TRIK_VIDTRANSCODE_CV_OV7670_InArgs and
+ * TRIK_VIDTRANSCODE_CV_OV7670_OutArgs (size fields checked): the sticky HSV
+ * range, the 4x4 metapixel bitmap, the clusterer and up to 8 targets by
+ * size, and the preview (set metapixels as 0x00ffff, guide lines, a 3x3 red
+ * mark per target).  Frames up to 2048x2048 (the reference: 640x480). */
+int32_t TRIK_VIDTRANSCODE_CV_create_ov7670(const TRIK_VIDTRANSCODE_CV_Params* params,
+                                           TRIK_VIDTRANSCODE_CV_Handle* out_handle);
 
 /* Replaces TRIK_VIDTRANSCODE_CV_free (WFXNS:114-136). */
 int32_t TRIK_VIDTRANSCODE_CV_delete(TRIK_VIDTRANSCODE_CV_Handle handle);
@@ -381,6 +435,30 @@ int32_t trik_hsv_line_preview(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvF
                               int32_t val_from, int32_t val_to, const TrikHsvTargetSums* sums_dev,
                               int32_t out_width, int32_t out_height, int32_t out_line_length,
                               uint8_t* previews_dev, int64_t preview_stride, void* hip_stream);
+
+/* The ov7670 multi-blob sensor for N ov7670 frames,
+ * one HSV range given as the InArgs centre/tolerance (converted as
+ * cv_bitmap_builder_reference.hpp:110-130):
+ *   targets_dev  [N][8] TrikHsvTarget: OutArgs target[i] (x, y, size; 0 when
+ *                not kept), OSEQ:563-590;
+ *   top_dev      optional [N][8][3] int32: size, sum_x, sum_y of the 8
+ *                largest clusters after the clusterer's postProcessing;
+ *   meta_dev     optional [N][H/4][W/4] uint8: 1 for set metapixels (more than
+ *                2 of 16 pixels detected);
+ *   labels_dev   optional [N][H/4][W/4] uint16: the clusterer's label map;
+ *   n_labels_dev optional [N] int32: labels including the background.
+ * Scratch lives in the handle. */
+int32_t trik_hsv_blob_batch(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvFrameBatch* batch,
+                            const TRIK_VIDTRANSCODE_CV_OV7670_InArgsAlg* hsv, TrikHsvTarget* targets_dev,
+                            int32_t* top_dev, uint8_t* meta_dev, uint16_t* labels_dev,
+                            int32_t* n_labels_dev, void* hip_stream);
+
+/* Its previews for N frames from meta_dev and top_dev of trik_hsv_blob_batch
+ * (OSEQ:387-420, 548-580). */
+int32_t trik_hsv_blob_preview(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvFrameBatch* batch,
+                              const uint8_t* meta_dev, const int32_t* top_dev, int32_t out_width,
+                              int32_t out_height, int32_t out_line_length, uint8_t* previews_dev,
+                              int64_t preview_stride, void* hip_stream);
 
 /* Fill batch->frames (device, writable) with synthetic frames; frame i of the
  * batch is global frame first_frame + i.  kind 0 = uniform random bytes,

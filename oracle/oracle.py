@@ -43,7 +43,7 @@ class Range(C.Structure):
 
 
 class BlobArgs(C.Structure):
-    """trik_oracle_blob_args: ov7670 object sensor InArgsAlg (ov7670 trik_vidtranscode_cv.h:44-53)."""
+    """trik_oracle_blob_args: ov7670 object sensor InArgsAlg (ov7670 trik_vidtranscode_cv.h:51-60)."""
     _fields_ = [("set_hsv_range", C.c_int32), ("hue", C.c_uint16), ("hue_tol", C.c_uint16),
                 ("sat", C.c_uint8), ("sat_tol", C.c_uint8), ("val", C.c_uint8), ("val_tol", C.c_uint8),
                 ("auto_detect", C.c_int32)]

@@ -174,7 +174,7 @@ int      trik_oracle_line_run(const uint8_t* frame, int64_t frame_size, int widt
  * (cv_clusterizer_reference.hpp:85-202, CLU). */
 
 /* TRIK_VIDTRANSCODE_CV_InArgsAlg of trik/ov7670/object_sensor/
- * trik_vidtranscode_cv.h:44-53 (XDAS_Bool restated as int32). */
+ * trik_vidtranscode_cv.h:51-60 (XDAS_Bool restated as int32). */
 typedef struct trik_oracle_blob_args {
   int32_t set_hsv_range;
   uint16_t hue, hue_tol;    /* 0..359 */

@@ -55,7 +55,21 @@ const TRIK_VIDTRANSCODE_CV_Params k_default_params = {{
 // LSEQ = trik/ov7670/line_sensor/include/internal/cv_line_detector_seqpass.hpp;
 // its glue trik/ov7670/line_sensor/src/vidtranscode_cv.cpp is WGLUE with
 // YUV422P input and a 240x320 default output).
-enum Algo { kAlgoBall = 0, kAlgoLine = 1 };
+enum Algo { kAlgoBall = 0, kAlgoLine = 1, kAlgoBlob = 2 };
+
+// ov7670 object sensor glue: the webcam glue with formatInput = YUV422P
+// (trik/ov7670/object_sensor/src/vidtranscode_cv.cpp:80,157)
+const TRIK_VIDTRANSCODE_CV_Params k_default_params_blob = {{
+    (int32_t)sizeof(TRIK_VIDTRANSCODE_CV_Params),
+    1,
+    TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_YUV422P,
+    {TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_RGB565X, TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_UNKNOWN},
+    480, 640, 60000, -1,
+    {480, -1},
+    {640, -1},
+    {-1, -1},
+    {-1, -1},
+    1 /* XDM_BYTE */}};
 
 const TRIK_VIDTRANSCODE_CV_Params k_default_params_line = {{
     (int32_t)sizeof(TRIK_VIDTRANSCODE_CV_Params),  // line glue :153-184
@@ -151,6 +165,19 @@ struct TrikCvHandle {
   size_t d_frame_cap = 0;
   TrikHsvTargetSums* d_sums = nullptr;
   TrikHsvTarget* d_targets = nullptr;
+
+  // ov7670 multi-blob sensor: BitmapBuilder's sticky range (uninitialised in
+  // the reference before the first setHsvRange; zero here) and scratch
+  PackedRange blob_range{0u, 0u, 0u};
+  uint8_t* d_meta = nullptr;
+  size_t d_meta_cap = 0;
+  int32_t* d_blob_stats = nullptr;
+  size_t d_blob_stats_cap = 0;
+  int32_t* d_blob_top = nullptr;
+  size_t d_blob_top_cap = 0;
+  TrikHsvTarget* d_blob_targets = nullptr;
+  size_t d_blob_targets_cap = 0;
+  hipEvent_t blob_busy = nullptr;
 };
 
 namespace {
@@ -172,6 +199,12 @@ void release(TrikCvHandle* h) {
   (void)hipFree(h->d_auto);
   (void)hipFree(h->d_sums);
   (void)hipFree(h->d_targets);
+  if (h->blob_busy) (void)hipEventSynchronize(h->blob_busy);
+  (void)hipFree(h->d_meta);
+  (void)hipFree(h->d_blob_stats);
+  (void)hipFree(h->d_blob_top);
+  (void)hipFree(h->d_blob_targets);
+  if (h->blob_busy) (void)hipEventDestroy(h->blob_busy);
   if (h->tables_busy) (void)hipEventDestroy(h->tables_busy);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   if (switched) (void)hipSetDevice(prev);
@@ -206,6 +239,9 @@ int32_t setup_image_desc(TrikCvHandle* h) {
   const bool out_ok = out_fmt == TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_RGB565X ||
                       (p.numOutputStreams == 0 && out_fmt == TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_UNKNOWN);
   int layout;
+  if (h->algo == kAlgoBlob &&
+      (in_w > 8192 || blob_max_labels(in_w / 4, in_h / 4) > 30000))  // uint16 labels, LDS
+    return fail(TRIK_IALG_EFAIL, "CV algorithm setup failed: frame too large for the multi-blob sensor");
   if (h->algo == kAlgoBall && in_fmt == TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_YUV422 && out_ok)
     layout = TRIK_HSV_LAYOUT_YUYV;
   else if (in_fmt == TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_YUV422P && out_ok)  // line: YUV422P only
@@ -382,6 +418,74 @@ LineArgs line_args(const TrikHsvFrameBatch& b, int val_from, int val_to, int ban
   return a;
 }
 
+// BitmapBuilder::run's range update (cv_bitmap_builder_reference.hpp:110-130):
+// from/to around the centre (hue wraps, sat/val clip), scaled as the webcam's,
+// then resetHsvRange (:62-77).
+int wrap_value(int v, int adj, int lo, int hi) {  // makeValueWrap, stdcpp.hpp
+  v += adj;
+  while (v > hi) v -= hi - lo + 1;
+  while (v < lo) v += hi - lo + 1;
+  return v;
+}
+int clip_value(int v, int adj, int lo, int hi) {  // makeValueRange, stdcpp.hpp
+  v += adj;
+  return v > hi ? hi : (v < lo ? lo : v);
+}
+PackedRange blob_pack(const TRIK_VIDTRANSCODE_CV_OV7670_InArgsAlg& a) {
+  TRIK_VIDTRANSCODE_CV_InArgsAlg r;
+  memset(&r, 0, sizeof r);
+  r.detectHueFrom = (uint16_t)wrap_value(a.detectHue, -(int)a.detectHueTol, 0, 359);
+  r.detectHueTo = (uint16_t)wrap_value(a.detectHue, (int)a.detectHueTol, 0, 359);
+  r.detectSatFrom = (uint8_t)clip_value(a.detectSat, -(int)a.detectSatTol, 0, 100);
+  r.detectSatTo = (uint8_t)clip_value(a.detectSat, (int)a.detectSatTol, 0, 100);
+  r.detectValFrom = (uint8_t)clip_value(a.detectVal, -(int)a.detectValTol, 0, 100);
+  r.detectValTo = (uint8_t)clip_value(a.detectVal, (int)a.detectValTol, 0, 100);
+  return pack_range(r);  // same scaling and wrap packing (WSEQ:425-445 = BMB:62-77)
+}
+
+template <typename T>
+int32_t grow(T*& p, size_t& cap, size_t bytes) {
+  if (bytes <= cap) return 0;
+  (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  HIP_TRY(hipMalloc(&p, bytes));
+  cap = bytes;
+  return 0;
+}
+
+// Scratch for n frames of W x H; waits for the previous blob work of the handle.
+int32_t ensure_blob_scratch(TrikCvHandle* h, int n, int w, int hgt) {
+  if (h->blob_busy) HIP_TRY(hipEventSynchronize(h->blob_busy));
+  const size_t bw = (size_t)(w / 4), bh = (size_t)(hgt / 4), nn = (size_t)(n > 0 ? n : 1);
+  const size_t ml = (size_t)blob_max_labels((int)bw, (int)bh);
+  int32_t r = grow(h->d_meta, h->d_meta_cap, nn * (bw * bh > 0 ? bw * bh : 1));
+  if (!r) r = grow(h->d_blob_stats, h->d_blob_stats_cap, nn * 6 * ml * sizeof(int32_t));
+  if (!r) r = grow(h->d_blob_top, h->d_blob_top_cap, nn * 24 * sizeof(int32_t));
+  if (!r) r = grow(h->d_blob_targets, h->d_blob_targets_cap, nn * 8 * sizeof(TrikHsvTarget));
+  return r;
+}
+
+BlobArgs blob_args(TrikCvHandle* h, const TrikHsvFrameBatch& b, PackedRange range, TrikHsvTarget* targets,
+                   int32_t* top, uint8_t* meta, uint16_t* labels, int32_t* n_labels) {
+  BlobArgs a;
+  a.frames = static_cast<const uint8_t*>(b.frames);
+  a.frame_stride = b.frame_stride;
+  a.n_frames = b.n_frames;
+  a.width = b.width; a.height = b.height; a.line_length = b.line_length;
+  a.range = range;
+  a.aligned4 = (reinterpret_cast<uintptr_t>(b.frames) & 3) == 0 && (b.n_frames <= 1 || (b.frame_stride & 3) == 0) &&
+               (b.line_length & 3) == 0;
+  a.meta = meta ? meta : h->d_meta;
+  a.labels = labels;
+  a.stats = h->d_blob_stats;
+  a.max_labels = (int32_t)blob_max_labels(b.width / 4, b.height / 4);
+  a.targets = targets ? targets : h->d_blob_targets;
+  a.top = top ? top : h->d_blob_top;
+  a.n_labels = n_labels;
+  return a;
+}
+
 AutoRangeArgs auto_range_args(const TrikHsvFrameBatch& b, uint16_t* out) {
   AutoRangeArgs a;
   a.frames = static_cast<const uint8_t*>(b.frames);
@@ -409,7 +513,9 @@ static int32_t create_handle(int algo, const TRIK_VIDTRANSCODE_CV_Params* params
     return fail(TRIK_IALG_EFAIL, "no HIP device");
   }
   h->algo = algo;
-  h->params = params ? *params : (algo == kAlgoLine ? k_default_params_line : k_default_params);  // WGLUE:188-191
+  h->params = params ? *params
+                     : (algo == kAlgoLine ? k_default_params_line
+                                          : (algo == kAlgoBlob ? k_default_params_blob : k_default_params));  // WGLUE:188-191
   const int32_t rc = setup_dynamic(h, nullptr);      // WFXNS:158-163
   if (rc != TRIK_IALG_EOK) {
     release(h);
@@ -427,6 +533,11 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_create(const TRIK_VIDTRANSCODE_CV_Params
 extern "C" int32_t TRIK_VIDTRANSCODE_CV_create_line(const TRIK_VIDTRANSCODE_CV_Params* params,
                                                     TRIK_VIDTRANSCODE_CV_Handle* out_handle) {
   return create_handle(kAlgoLine, params, out_handle);
+}
+
+extern "C" int32_t TRIK_VIDTRANSCODE_CV_create_ov7670(const TRIK_VIDTRANSCODE_CV_Params* params,
+                                                      TRIK_VIDTRANSCODE_CV_Handle* out_handle) {
+  return create_handle(kAlgoBlob, params, out_handle);
 }
 
 extern "C" int32_t TRIK_VIDTRANSCODE_CV_delete(TRIK_VIDTRANSCODE_CV_Handle handle) {
@@ -489,8 +600,13 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
   if (!h || !in_bufs || !out_bufs || !in_args || !out_args)
     return fail(TRIK_IVIDTRANSCODE_EFAIL, "NULL argument");
   std::lock_guard<std::mutex> lock(h->mu);
-  if (in_args->base.size != (int32_t)sizeof(TRIK_VIDTRANSCODE_CV_InArgs) ||  // WFXNS:192-197
-      out_args->base.size != (int32_t)sizeof(TRIK_VIDTRANSCODE_CV_OutArgs)) {
+  const bool blob = h->algo == kAlgoBlob;  // the ov7670 object sensor's own InArgs / OutArgs
+  const int32_t in_want = blob ? (int32_t)sizeof(TRIK_VIDTRANSCODE_CV_OV7670_InArgs)
+                               : (int32_t)sizeof(TRIK_VIDTRANSCODE_CV_InArgs);
+  const int32_t out_want = blob ? (int32_t)sizeof(TRIK_VIDTRANSCODE_CV_OV7670_OutArgs)
+                                : (int32_t)sizeof(TRIK_VIDTRANSCODE_CV_OutArgs);
+  if (in_args->base.size != in_want ||  // WFXNS:192-197
+      out_args->base.size != out_want) {
     set_bit(out_args->base.extendedError, TRIK_XDM_UNSUPPORTEDPARAM_BIT);
     return fail(TRIK_IVIDTRANSCODE_EUNSUPPORTED, "InArgs/OutArgs size mismatch");
   }
@@ -538,7 +654,13 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
   if (rc == TRIK_IVIDTRANSCODE_EOK) {
     out_size = (int64_t)h->out_h * h->out_ll;  // WSEQ:419
     TRIK_VIDTRANSCODE_CV_OutArgsAlg& oa = out_args->alg;
-    oa.targetX = 0; oa.targetY = 0; oa.targetSize = 0;
+    auto* ia7 = reinterpret_cast<const TRIK_VIDTRANSCODE_CV_OV7670_InArgs*>(in_args);
+    auto* oa7 = reinterpret_cast<TRIK_VIDTRANSCODE_CV_OV7670_OutArgs*>(out_args);
+    if (blob)
+      memset(oa7->alg.target, 0, sizeof oa7->alg.target);  // OSEQ:563
+    else {
+      oa.targetX = 0; oa.targetY = 0; oa.targetSize = 0;
+    }
     if (h->in_w > 0 && h->in_h > 0) {
       int prev = 0;
       const bool switched = hipGetDevice(&prev) == hipSuccess && prev != h->device;
@@ -557,6 +679,38 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
         HIP_TRY(hipMemcpyAsync(h->d_frame, in->buf, fb, hipMemcpyHostToDevice, h->stream));
         TrikHsvFrameBatch b = {h->d_frame, (int64_t)fb, 1, h->in_w, h->in_h, h->in_ll, h->layout};
         HIP_TRY(hipMemsetAsync(h->d_sums, 0, sizeof(TrikHsvTargetSums), h->stream));
+        if (blob) {  // BallDetector<YUV422P>::run, OSEQ:516-602
+          if (ia7->alg.setHsvRange) h->blob_range = blob_pack(ia7->alg);  // BMB:110-130
+          int32_t r = ensure_blob_scratch(h, 1, h->in_w, h->in_h);
+          if (r) return r;
+          const BlobArgs ba = blob_args(h, b, h->blob_range, nullptr, nullptr, nullptr, nullptr, nullptr);
+          HIP_TRY(launch_blob(ba, h->stream));
+          if (out_ptr && out_size > 0) {  // preview: set metapixels, guide lines, target marks
+            const size_t pb = (size_t)out_size;
+            r = grow(h->d_preview, h->d_preview_cap, pb);
+            if (r) return r;
+            r = ensure_maps(h, h->in_w, h->in_h, h->out_w, h->out_h, h->stream);
+            if (r) return r;
+            TRIK_VIDTRANSCODE_CV_InArgsAlg none;
+            memset(&none, 0, sizeof none);
+            PreviewArgs pa = preview_args(h, b, none, h->out_w, h->out_h, h->out_ll, h->d_preview, (int64_t)pb);
+            pa.meta = ba.meta;
+            HIP_TRY(launch_preview_body(pa, h->stream));
+            HIP_TRY(launch_blob_overlay(pa, ba.top, h->stream));
+            HIP_TRY(hipMemcpyAsync(out_ptr, h->d_preview, pb, hipMemcpyDeviceToHost, h->stream));
+          }
+          TrikHsvTarget t[8];
+          HIP_TRY(hipMemcpyAsync(t, ba.targets, sizeof t, hipMemcpyDeviceToHost, h->stream));
+          HIP_TRY(hipStreamSynchronize(h->stream));
+          for (int i = 0; i < 8; ++i) {
+            oa7->alg.target[i].x = t[i].x;
+            oa7->alg.target[i].y = t[i].y;
+            oa7->alg.target[i].size = t[i].size;
+          }
+          // autoDetectHsv: the ov7670 range detector is a simulated annealing
+          // seeded by srand(time(NULL)) -- not reproducible; detect* untouched.
+          return 0;
+        }
         if (h->algo == kAlgoLine) {  // LineDetector::run, LSEQ:376-476
           const TRIK_VIDTRANSCODE_CV_InArgsAlg& ia = in_args->alg;
           HIP_TRY(launch_line(line_args(b, ia.detectValFrom, ia.detectValTo, h->line_band[0],
@@ -795,6 +949,69 @@ extern "C" int32_t trik_hsv_line_preview(TRIK_VIDTRANSCODE_CV_Handle h, const Tr
   pa.range = line_range(val_from, val_to);
   HIP_TRY(launch_preview_body(pa, s));
   HIP_TRY(launch_line_overlay(pa, sums, s));
+  if (!h->tables_busy) HIP_TRY(hipEventCreateWithFlags(&h->tables_busy, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(h->tables_busy, s));
+  return 0;
+}
+
+extern "C" int32_t trik_hsv_blob_batch(TRIK_VIDTRANSCODE_CV_Handle h, const TrikHsvFrameBatch* b,
+                                       const TRIK_VIDTRANSCODE_CV_OV7670_InArgsAlg* hsv, TrikHsvTarget* targets,
+                                       int32_t* top, uint8_t* meta, uint16_t* labels, int32_t* n_labels,
+                                       void* stream) {
+  if (!h) return fail(TRIK_IVIDTRANSCODE_EFAIL, "handle is NULL");
+  const std::string e = validate_batch(b);
+  if (!e.empty()) return fail(TRIK_IVIDTRANSCODE_EFAIL, e);
+  if (b->layout != TRIK_HSV_LAYOUT_OV7670)
+    return fail(TRIK_IVIDTRANSCODE_EFAIL, "the multi-blob sensor takes the ov7670 layout (YUV422P)");
+  if (!hsv) return fail(TRIK_IVIDTRANSCODE_EFAIL, "hsv is NULL");
+  if (b->width % 32 || b->height % 4) return fail(TRIK_IVIDTRANSCODE_EFAIL, "width % 32 / height % 4");
+  if (b->width > 8192 || blob_max_labels(b->width / 4, b->height / 4) > 30000)
+    return fail(TRIK_IVIDTRANSCODE_EFAIL, "frame too large for the multi-blob sensor");
+  if (b->n_frames > 0 && !targets) return fail(TRIK_IVIDTRANSCODE_EFAIL, "targets is NULL");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  std::lock_guard<std::mutex> lock(h->mu);
+  if (b->n_frames == 0) return 0;
+  if (b->width == 0 || b->height == 0) {
+    HIP_TRY(hipMemsetAsync(targets, 0, sizeof(TrikHsvTarget) * 8 * (size_t)b->n_frames, s));
+    if (top) HIP_TRY(hipMemsetAsync(top, 0, sizeof(int32_t) * 24 * (size_t)b->n_frames, s));
+    if (n_labels) HIP_TRY(hipMemsetAsync(n_labels, 0, sizeof(int32_t) * (size_t)b->n_frames, s));
+    return 0;
+  }
+  int32_t r = ensure_blob_scratch(h, b->n_frames, b->width, b->height);
+  if (r) return r;
+  const BlobArgs ba = blob_args(h, *b, blob_pack(*hsv), targets, top, meta, labels, n_labels);
+  HIP_TRY(launch_blob(ba, s));
+  if (!h->blob_busy) HIP_TRY(hipEventCreateWithFlags(&h->blob_busy, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(h->blob_busy, s));
+  return 0;
+}
+
+extern "C" int32_t trik_hsv_blob_preview(TRIK_VIDTRANSCODE_CV_Handle h, const TrikHsvFrameBatch* b,
+                                         const uint8_t* meta, const int32_t* top, int32_t out_width,
+                                         int32_t out_height, int32_t out_line_length, uint8_t* previews,
+                                         int64_t preview_stride, void* stream) {
+  if (!h) return fail(TRIK_IVIDTRANSCODE_EFAIL, "handle is NULL");
+  const std::string e = validate_batch(b);
+  if (!e.empty()) return fail(TRIK_IVIDTRANSCODE_EFAIL, e);
+  if (b->layout != TRIK_HSV_LAYOUT_OV7670)
+    return fail(TRIK_IVIDTRANSCODE_EFAIL, "the multi-blob sensor takes the ov7670 layout (YUV422P)");
+  if (out_width < 0 || out_height < 0 || out_line_length < 2 * out_width)
+    return fail(TRIK_IVIDTRANSCODE_EFAIL, "preview geometry: need out_line_length >= 2*out_width");
+  const int64_t pb = (int64_t)out_height * out_line_length;
+  if (b->n_frames > 1 && preview_stride < pb)
+    return fail(TRIK_IVIDTRANSCODE_EFAIL, "preview_stride smaller than one preview");
+  if (b->n_frames > 0 && pb > 0 && (!previews || !meta || !top)) return fail(TRIK_IVIDTRANSCODE_EFAIL, "NULL buffer");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  std::lock_guard<std::mutex> lock(h->mu);
+  if (b->n_frames == 0 || pb == 0) return 0;
+  int32_t rc = ensure_maps(h, b->width, b->height, out_width, out_height, s);
+  if (rc) return rc;
+  TRIK_VIDTRANSCODE_CV_InArgsAlg none;
+  memset(&none, 0, sizeof none);
+  PreviewArgs pa = preview_args(h, *b, none, out_width, out_height, out_line_length, previews, preview_stride);
+  pa.meta = meta;
+  HIP_TRY(launch_preview_body(pa, s));
+  HIP_TRY(launch_blob_overlay(pa, top, s));
   if (!h->tables_busy) HIP_TRY(hipEventCreateWithFlags(&h->tables_busy, hipEventDisableTiming));
   HIP_TRY(hipEventRecord(h->tables_busy, s));
   return 0;

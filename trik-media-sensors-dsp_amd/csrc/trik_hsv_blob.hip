@@ -1,0 +1,374 @@
+// trik_hsv_blob.hip -- the ov7670 multi-blob object sensor (SURVEY 8(f) row
+// 3).  OSEQ = trik/ov7670/object_sensor/include/internal/
+// cv_ball_detector_seqpass.hpp, BMB = .../cv_bitmap_builder_reference.hpp,
+// CLU = .../cv_clusterizer_reference.hpp.
+//
+//  blob_meta_kernel  per-pixel HSV + the sticky range, counted per 4x4
+//                    metapixel (BMB:171-190); set when more than 2 of 16
+//                    (CLU:185-186).  A lane per (metapixel, row of it): four
+//                    lanes sum with two xor-shuffles.
+//  blob_ccl_kernel   Clusterizer::run + postProcessing + the target epilogue,
+//                    one wave per frame, reproducing the reference's
+//                    sequential scan exactly:
+//    * labels: a set metapixel takes the smallest non-zero label among left,
+//      up-left, up and up-right (CLU:44-52, 70-84), else a new one.  Which
+//      metapixels open labels depends only on the bitmap (no set causal
+//      neighbour), so new labels are numbered by a prefix sum; along a row,
+//      labels are a prefix minimum over runs of set metapixels of the
+//      up-row minima -- one segmented min-scan per row across the wave;
+//    * statistics: every non-opening set metapixel adds (c, r, 1) to its
+//      label (CLU:91-95; the opening one is not counted, CLU:98-112), with
+//      one atomic per run of equal labels in a lane;
+//    * equivalences: eq[a] = eq[L] for each non-zero neighbour a (equal to
+//      the reference's conditional form, CLU:92-96), in raster order; only
+//      metapixels with a neighbour label other than L can change anything,
+//      and they are replayed serially by the owning lane, lane by lane;
+//    * postProcessing (CLU:115-127), order-free: label k ends with its own
+//      x, y (size only if eq[k] == k) plus the own sums of every j with
+//      eq[j] == k, j != k (eq[j] <= j, so j's sums are final when folded);
+//    * the 8 largest by size, ties by label (std::sort's order among equals
+//      is unspecified in the reference), and OSEQ:563-590's arithmetic.
+//  blob_overlay_kernel  guide lines, then a 3x3 red mark per kept target.
+#include <hip/hip_runtime.h>
+
+#include "trik_hsv_internal.h"
+#include "trik_hsv_pixel.h"
+
+namespace trik_hsv {
+
+namespace {
+
+constexpr int kMetaCols = 64;  // metapixel columns per 256-lane workgroup
+
+__global__ __launch_bounds__(256) void blob_meta_kernel(BlobArgs a) {
+  __shared__ uint16_t l43[256], l255[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {  // OSEQ:489-499
+    l43[i] = i ? (uint16_t)((43u * 256u) / (uint32_t)i) : 0;
+    l255[i] = i ? (uint16_t)((255u * 256u) / (uint32_t)i) : 0;
+  }
+  __syncthreads();
+  const int bw = a.width >> 2, bh = a.height >> 2;
+  const int chunks = (bw + kMetaCols - 1) / kMetaCols;
+  const int per_frame = bh * chunks;
+  const int f = blockIdx.x / per_frame;
+  const int rem = blockIdx.x - f * per_frame;
+  const int mr = rem / chunks;
+  const int mc = (rem - mr * chunks) * kMetaCols + (threadIdx.x >> 2);
+  const int rr = threadIdx.x & 3;
+  uint32_t cnt = 0;
+  if (mc < bw) {
+    const int64_t ll = a.line_length;
+    const uint8_t* yp = a.frames + (int64_t)f * a.frame_stride + (int64_t)(4 * mr + rr) * ll + 4 * mc;
+    const uint8_t* cp = yp + (int64_t)a.height * ll;
+    uint32_t yw, cw;
+    if (a.aligned4) {
+      yw = *reinterpret_cast<const uint32_t*>(yp);
+      cw = *reinterpret_cast<const uint32_t*>(cp);
+    } else {
+      yw = (uint32_t)yp[0] | ((uint32_t)yp[1] << 8) | ((uint32_t)yp[2] << 16) | ((uint32_t)yp[3] << 24);
+      cw = (uint32_t)cp[0] | ((uint32_t)cp[1] << 8) | ((uint32_t)cp[2] << 16) | ((uint32_t)cp[3] << 24);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // chroma V0 U0 V1 U1: V even, U odd (OSEQ:369-373)
+      const int sh = 16 * (k >> 1);
+      const PixelRgb p = pixel_rgb((int)((yw >> (8 * k)) & 0xFFu), (int)((cw >> (sh + 8)) & 0xFFu),
+                                   (int)((cw >> sh) & 0xFFu));
+      uint32_t H, S, V;
+      pixel_hsv_bytes(p, l43, l255, H, S, V);
+      cnt += detect_packed(H, S, V, a.range) ? 1u : 0u;
+    }
+  }
+  cnt += __shfl_xor(cnt, 1, 64);
+  cnt += __shfl_xor(cnt, 2, 64);
+  if (rr == 0 && mc < bw) a.meta[((int64_t)f * bh + mr) * bw + mc] = cnt > 2 ? 1 : 0;
+}
+
+constexpr uint32_t kInf = 0xFFFFu;
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t o = __shfl_xor(v, off, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+// OSEQ:563-590 for one cluster: kept when the size percentage exceeds 4;
+// (x, y) = the mark's source point (getX/getY, CLU:139-147).
+__device__ __forceinline__ bool blob_target(int32_t size, int32_t sx, int32_t sy, int bw, int bh, int& pct,
+                                            int32_t& x, int32_t& y) {
+  const int root = (int)__fsqrt_rn((float)(uint16_t)size);  // getSize() is uint16_t
+  const uint32_t radius = (uint32_t)ceilf(__fdiv_rn((float)root, 3.1415927f));
+  pct = (int)((radius * 100u * 4u) / (uint32_t)(bw + bh));
+  if (pct <= 4) return false;
+  x = (sx / (size + 1)) * 4;
+  y = (sy / (size + 1)) * 4;
+  return true;
+}
+
+__global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
+  extern __shared__ uint16_t smem[];
+  const int f = blockIdx.x, lane = threadIdx.x;
+  const int bw = a.width >> 2, bh = a.height >> 2;
+  const int ml = a.max_labels;
+  uint16_t* eq = smem;                          // [ml]
+  uint16_t* prev = eq + ((ml + 1) & ~1);        // [bw] labels of row r-1
+  uint16_t* cur = prev + bw;                    // [bw] labels of row r
+  uint16_t* up = cur + bw;                      // [bw] up-row minimum, kInf if none
+  uint8_t* dset = reinterpret_cast<uint8_t*>(up + bw);  // [bw] set flags of row r
+  const uint8_t* meta = a.meta + (int64_t)f * bw * bh;
+  int32_t* own = a.stats + (int64_t)f * 2 * 3 * ml;  // own[3k + {0,1,2}] = x, y, size
+  int32_t* fin = own + 3 * ml;
+  uint16_t* labels = a.labels ? a.labels + (int64_t)f * bw * bh : nullptr;
+
+  const int K = (bw + 63) / 64;  // columns per lane, contiguous
+  const int c0 = lane * K, c1 = min(c0 + K, bw);
+  for (int c = lane; c < bw; c += 64) prev[c] = 0;
+  if (lane == 0) eq[0] = 0;
+  int next = 1;  // next new label (wave-uniform)
+  for (int r = 0; r < bh; ++r) {
+    // phase 1: set flags and up-row minima (CLU:70-84)
+    for (int c = lane; c < bw; c += 64) {
+      const uint8_t d = meta[(int64_t)r * bw + c];
+      dset[c] = d;
+      uint32_t u = kInf;
+      if (d && r > 0) {
+        const uint32_t p0 = c > 0 ? prev[c - 1] : 0u, p1 = prev[c], p2 = c < bw - 1 ? prev[c + 1] : 0u;
+        if (p0) u = p0;
+        if (p1 && p1 < u) u = p1;
+        if (p2 && p2 < u) u = p2;
+      }
+      up[c] = (uint16_t)u;
+    }
+    __syncthreads();
+    // phase 2: opening metapixels (set, no set causal neighbour) get new labels
+    // numbered in raster order: an exclusive prefix sum of the lanes' counts
+    uint32_t nseed = 0;
+    for (int c = c0; c < c1; ++c)
+      if (dset[c] && !(c > 0 && dset[c - 1]) && up[c] == kInf) ++nseed;
+    uint32_t incl = nseed;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t o = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += o;
+    }
+    const uint32_t total = __shfl(incl, 63, 64);
+    const uint32_t label_next = (uint32_t)next + incl - nseed;
+    // segmented min-scan over runs of set metapixels: this lane's summary is
+    // (the chunk holds an unset one, the minimum after the last unset one)
+    uint32_t cb = 0, cm = kInf;
+    {
+      uint32_t lbl = label_next;
+      for (int c = c0; c < c1; ++c) {
+        if (!dset[c]) {
+          cb = 1;
+          cm = kInf;
+        } else {
+          const bool open = !(c > 0 && dset[c - 1]) && up[c] == kInf;
+          cm = min(cm, open ? lbl++ : (uint32_t)up[c]);
+        }
+      }
+    }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {  // inclusive scan of (break, min) pairs
+      const uint32_t ob = __shfl_up(cb, off, 64), om = __shfl_up(cm, off, 64);
+      if (lane >= off) {
+        cm = cb ? cm : min(om, cm);
+        cb = cb | ob;
+      }
+    }
+    uint32_t carry = __shfl_up(cm, 1, 64);  // exclusive: lanes before this one
+    if (lane == 0) carry = kInf;
+    // phase 3: labels; open the new labels (eq[L] = L, zero sums)
+    {
+      uint32_t lbl = label_next, run = carry;
+      for (int c = c0; c < c1; ++c) {
+        const bool d = dset[c] != 0;
+        const bool left = c > 0 && dset[c - 1] != 0;
+        if (!d) {
+          run = kInf;
+          cur[c] = 0;
+          continue;
+        }
+        if (!left && up[c] == kInf) {  // CLU:98-112
+          eq[lbl] = (uint16_t)lbl;
+          own[3 * lbl] = 0;
+          own[3 * lbl + 1] = 0;
+          own[3 * lbl + 2] = 0;
+          run = lbl++;
+        } else {
+          run = min(run, (uint32_t)up[c]);
+        }
+        cur[c] = (uint16_t)run;
+      }
+    }
+    next += (int)total;
+    __threadfence_block();
+    __threadfence();
+    __syncthreads();
+    // phase 4: statistics of the non-opening metapixels, one atomic per run of
+    // equal labels; equivalence events flagged
+    uint32_t events = 0;  // bit j: column c0 + j has a neighbour label != L
+    {
+      uint32_t acc_l = 0;
+      int32_t ax = 0, ay = 0, an = 0;
+      for (int c = c0; c < c1; ++c) {
+        const uint32_t L = cur[c];
+        const bool seed = L != 0 && !(c > 0 && dset[c - 1]) && up[c] == kInf;
+        if (L && !seed) {
+          if (L != acc_l) {
+            if (an) {
+              atomicAdd(&own[3 * acc_l], ax);
+              atomicAdd(&own[3 * acc_l + 1], ay);
+              atomicAdd(&own[3 * acc_l + 2], an);
+            }
+            acc_l = L;
+            ax = ay = an = 0;
+          }
+          ax += c;
+          ay += r;
+          ++an;
+          const uint32_t n0 = c > 0 ? cur[c - 1] : 0u;
+          const uint32_t n1 = (r > 0 && c > 0) ? prev[c - 1] : 0u;
+          const uint32_t n2 = r > 0 ? prev[c] : 0u;
+          const uint32_t n3 = (r > 0 && c < bw - 1) ? prev[c + 1] : 0u;
+          if ((n0 && n0 != L) || (n1 && n1 != L) || (n2 && n2 != L) || (n3 && n3 != L))
+            events |= 1u << (c - c0);
+        }
+        if (labels) labels[(int64_t)r * bw + c] = (uint16_t)L;
+      }
+      if (an) {
+        atomicAdd(&own[3 * acc_l], ax);
+        atomicAdd(&own[3 * acc_l + 1], ay);
+        atomicAdd(&own[3 * acc_l + 2], an);
+      }
+    }
+    // equivalence events in raster order: lane by lane, each lane in column order
+    uint64_t pending = __ballot(events != 0);
+    while (pending) {
+      const int l = __ffsll((unsigned long long)pending) - 1;
+      pending &= pending - 1;
+      if (lane == l) {
+        for (uint32_t ev = events; ev; ev &= ev - 1) {
+          const int c = c0 + __ffs(ev) - 1;
+          const uint32_t L = cur[c];
+          const uint16_t e = eq[L];
+          const uint32_t nb[4] = {c > 0 ? cur[c - 1] : 0u, (r > 0 && c > 0) ? prev[c - 1] : 0u,
+                                  r > 0 ? prev[c] : 0u, (r > 0 && c < bw - 1) ? prev[c + 1] : 0u};
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (nb[i]) eq[nb[i]] = e;  // CLU:92-96
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    uint16_t* t = prev;
+    prev = cur;
+    cur = t;
+  }
+  __threadfence();
+  __syncthreads();
+  const int n = next;
+  // postProcessing (CLU:115-127) without its order: fold own sums into fin
+  for (int k = lane; k < n; k += 64) {
+    if (k == 0) {
+      fin[0] = fin[1] = fin[2] = 0;
+      continue;
+    }
+    fin[3 * k] = own[3 * k];
+    fin[3 * k + 1] = own[3 * k + 1];
+    fin[3 * k + 2] = eq[k] == k ? own[3 * k + 2] : 0;
+  }
+  __threadfence();
+  __syncthreads();
+  for (int k = lane + 0; k < n; k += 64) {
+    const int e = eq[k];
+    if (k != 0 && e != k) {
+      atomicAdd(&fin[3 * e], own[3 * k]);
+      atomicAdd(&fin[3 * e + 1], own[3 * k + 1]);
+      atomicAdd(&fin[3 * e + 2], own[3 * k + 2]);
+    }
+  }
+  __threadfence();
+  __syncthreads();
+  // the 8 largest (size desc, label asc): key = size << 32 | ~label
+  uint64_t last = ~0ull;
+  int32_t* top = a.top + (int64_t)f * 24;
+  TrikHsvTarget* tg = a.targets + (int64_t)f * 8;
+  for (int i = 0; i < 8; ++i) {
+    uint64_t best = 0;
+    for (int k = lane; k < n; k += 64) {
+      const uint64_t key = ((uint64_t)(uint32_t)fin[3 * k + 2] << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)k);
+      if (key < last && key > best) best = key;
+    }
+    best = wave_max_u64(best);
+    last = best;
+    if (lane == 0) {
+      int32_t size = 0, sx = 0, sy = 0;
+      if (best) {
+        const uint32_t k = 0xFFFFFFFFu - (uint32_t)best;
+        size = fin[3 * k + 2];
+        sx = fin[3 * k];
+        sy = fin[3 * k + 1];
+      }
+      top[3 * i] = size;
+      top[3 * i + 1] = sx;
+      top[3 * i + 2] = sy;
+      TrikHsvTarget t = {0, 0, 0, 0};
+      int pct;
+      int32_t x, y;
+      if (best && blob_target(size, sx, sy, bw, bh, pct, x, y)) {  // OSEQ:574-583
+        t.size = (uint8_t)pct;
+        t.x = (int8_t)(((x - a.width / 2) * 100 * 2) / a.width);
+        t.y = (int8_t)(((y - a.height / 2) * 100 * 2) / a.height);
+      }
+      tg[i] = t;
+    }
+  }
+  if (lane == 0 && a.n_labels) a.n_labels[f] = n;
+}
+
+__global__ __launch_bounds__(64) void blob_overlay_kernel(PreviewArgs a, const int32_t* top) {
+  const int f = blockIdx.x, lane = threadIdx.x;
+  const Canvas cv{a.previews + (int64_t)f * a.preview_stride, a.out_ll, a.width, a.height, a.wi2wo, a.hi2ho};
+  draw_guides(cv, lane, 64);  // OSEQ:548-561
+  __syncthreads();
+  // drawFatPixel (OSEQ:92-108) per kept target, in target order: lane 9*i + j
+  // draws point j of target i; marks may overlap, so targets go in order
+  const int32_t* t = top + (int64_t)f * 24;
+  const int bw = a.width >> 2, bh = a.height >> 2;
+  for (int i = 0; i < 8; ++i) {
+    int pct;
+    int32_t x, y;
+    if (blob_target(t[3 * i], t[3 * i + 1], t[3 * i + 2], bw, bh, pct, x, y) && lane < 9)
+      cv.px(x + lane / 3 - 1, y + lane % 3 - 1, 0xff0000);
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+int launch_blob(const BlobArgs& a, hipStream_t s) {
+  if (a.n_frames <= 0 || a.width <= 0 || a.height <= 0) return hipSuccess;
+  const int bw = a.width >> 2, bh = a.height >> 2;
+  if (bw > 64 * 32) return hipErrorInvalidValue;  // events mask: 32 columns per lane
+  const int64_t mblocks = (int64_t)a.n_frames * bh * ((bw + kMetaCols - 1) / kMetaCols);
+  if (mblocks > 0x7FFFFFFF) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(blob_meta_kernel, dim3((unsigned)mblocks), dim3(256), 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const size_t lds = sizeof(uint16_t) * ((size_t)((a.max_labels + 1) & ~1) + 3 * (size_t)bw) + (size_t)bw;
+  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(blob_ccl_kernel, dim3((unsigned)a.n_frames), dim3(64), lds, s, a);
+  return hipGetLastError();
+}
+
+int launch_blob_overlay(const PreviewArgs& a, const int32_t* top, hipStream_t s) {
+  if (a.n_frames <= 0 || a.width <= 0 || a.height <= 0) return hipSuccess;
+  hipLaunchKernelGGL(blob_overlay_kernel, dim3((unsigned)a.n_frames), dim3(64), 0, s, a, top);
+  return hipGetLastError();
+}
+
+}  // namespace trik_hsv

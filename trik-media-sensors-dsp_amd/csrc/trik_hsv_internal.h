@@ -88,6 +88,9 @@ struct PreviewArgs {
   const int32_t* last_col;  // [out_w]
   const uint32_t* wi2wo;    // [width]  WSEQ:375-379
   const uint32_t* hi2ho;    // [height] WSEQ:381-385
+  // ov7670 multi-blob preview: when set, a pixel is "detected" iff its 4x4
+  // metapixel is set ([n][H/4][W/4], OSEQ:411-413) instead of by `range`
+  const uint8_t* meta = nullptr;
 };
 
 // Auto HSV range of N frames (trik_hsv_operator.hip); out[f][6] = detectHue,
@@ -129,6 +132,29 @@ int launch_line(const LineArgs& a, hipStream_t s);
 // preview body as launch_preview's first kernel, then the line sensor's overlay
 int launch_preview_body(const PreviewArgs& a, hipStream_t s);
 int launch_line_overlay(const PreviewArgs& a, const TrikHsvTargetSums* sums, hipStream_t s);
+
+// ov7670 multi-blob sensor of N frames (trik_hsv_blob.hip).
+struct BlobArgs {
+  const uint8_t* frames;
+  int64_t frame_stride;
+  int32_t n_frames, width, height, line_length;
+  PackedRange range;         // the sticky BitmapBuilder range (BMB:62-77)
+  int32_t aligned4;          // frames, stride and line length 4-byte aligned
+  uint8_t* meta;             // [n][H/4][W/4]: 1 for set metapixels
+  uint16_t* labels;          // optional [n][H/4][W/4]: the clusterer's label map
+  int32_t* stats;            // scratch [n][2][max_labels][3]: own and folded {x, y, size}
+  int32_t max_labels;        // blob_max_labels(W/4, H/4)
+  TrikHsvTarget* targets;    // [n][8]
+  int32_t* top;              // [n][8][3]: size, sum_x, sum_y of the 8 largest clusters
+  int32_t* n_labels;         // optional [n]
+};
+// Labels a frame can need: seeds are pairwise non-adjacent in the 8-neighbourhood
+// (a metapixel next to an earlier set one is never a seed), so at most
+// ceil(bw/2) * ceil(bh/2) of them, plus the background label 0.
+inline int64_t blob_max_labels(int bw, int bh) { return (int64_t)((bw + 1) / 2) * ((bh + 1) / 2) + 1; }
+int launch_blob(const BlobArgs& a, hipStream_t s);
+// guide lines + a 3x3 mark per kept target (OSEQ:548-580), from BlobArgs.top
+int launch_blob_overlay(const PreviewArgs& a, const int32_t* top, hipStream_t s);
 
 // Host side of the preview geometry (trik_hsv_tables.cpp): the reference's
 // scale maps and their inverses, packed as

@@ -238,12 +238,6 @@ __global__ void line_targets_kernel(int n_frames, int width, int height, const T
   targets[f] = t;
 }
 
-__device__ __forceinline__ void write_px565(uint8_t* dst, uint32_t rgb888) {
-  const uint32_t v = ((rgb888 >> 19) & 0x001fu) | ((rgb888 >> 5) & 0x07e0u) | ((rgb888 << 8) & 0xf800u);
-  dst[0] = (uint8_t)v;
-  dst[1] = (uint8_t)(v >> 8);
-}
-
 __global__ __launch_bounds__(64) void line_overlay_kernel(PreviewArgs a, const TrikHsvTargetSums* sums) {
   const int f = blockIdx.x, lane = threadIdx.x;
   uint8_t* out = a.previews + (int64_t)f * a.preview_stride;

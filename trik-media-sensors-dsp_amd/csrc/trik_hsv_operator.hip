@@ -43,26 +43,15 @@ constexpr Luts make_luts() {  // WSEQ:400-406
 }
 __constant__ Luts c_luts = make_luts();
 
-// writeOutputPixel, WSEQ:66-70: 0x00RRGGBB -> B5 G6 R5 (R in the low bits),
-// little-endian bytes (the output line length need not be even).
-__device__ __forceinline__ void write_px(uint8_t* dst, uint32_t rgb888) {
-  const uint32_t v = ((rgb888 >> 19) & 0x001fu) | ((rgb888 >> 5) & 0x07e0u) | ((rgb888 << 8) & 0xf800u);
-  dst[0] = (uint8_t)v;
-  dst[1] = (uint8_t)(v >> 8);
-}
 
-// detectHsvPixel (WSEQ:171-179) for one packed range: per-byte "outside the
-// bounds" bits compared with the expected pattern (1 for a wrapped hue).
-__device__ __forceinline__ bool detect_packed(uint32_t H, uint32_t S, uint32_t V, const PackedRange& r) {
-  const uint32_t out = ((H < (r.from & 0xFFu)) | (H > (r.to & 0xFFu))) |
-                       (((S < ((r.from >> 8) & 0xFFu)) | (S > ((r.to >> 8) & 0xFFu))) << 1) |
-                       (((V < ((r.from >> 16) & 0xFFu)) | (V > ((r.to >> 16) & 0xFFu))) << 2);
-  return out == r.expect;
-}
-
-// One pixel of the preview: RGB565X of (det ? 0x00ffff : rgb888), WSEQ:347.
-__device__ __forceinline__ uint32_t preview_px(int Y, int U, int V, const PackedRange& range) {
+// One pixel of the preview: RGB565X of (det ? 0x00ffff : rgb888), WSEQ:347;
+// det from the range, or from the metapixel flag when meta_det >= 0 (OSEQ:411-413).
+__device__ __forceinline__ uint32_t preview_px(int Y, int U, int V, const PackedRange& range, int meta_det) {
   const PixelRgb p = pixel_rgb(Y, U, V);
+  if (meta_det >= 0) {
+    const uint32_t rgb = meta_det ? 0x00ffffu : p.rgb888();
+    return ((rgb >> 19) & 0x001fu) | ((rgb >> 5) & 0x07e0u) | ((rgb << 8) & 0xf800u);
+  }
   const int mx = max(p.r, max(p.g, p.b)), mn = min(p.r, min(p.g, p.b));
   const int m = c_luts.l43[mx - mn];
   int h;
@@ -106,7 +95,9 @@ __global__ __launch_bounds__(64 * kPreviewRows) void preview_kernel(PreviewArgs 
     } else {
       fetch_yuv(fr, a.height, a.line_length, a.layout, sr, sc, Y, U, V);
     }
-    v[k] = preview_px(Y, U, V, a.range);
+    const int meta_det =
+        a.meta ? (int)a.meta[((int64_t)f * (a.height >> 2) + (sr >> 2)) * (a.width >> 2) + (sc >> 2)] : -1;
+    v[k] = preview_px(Y, U, V, a.range, meta_det);
   }
   const int b0 = 4 * q;
   if (a.aligned4 && b0 + 4 <= a.out_ll) {
@@ -118,19 +109,6 @@ __global__ __launch_bounds__(64 * kPreviewRows) void preview_kernel(PreviewArgs 
   }
 }
 
-struct Canvas {
-  uint8_t* out;
-  int out_ll, width, height;
-  const uint32_t* wi2wo;
-  const uint32_t* hi2ho;
-  // drawOutputPixelBound, WSEQ:72-89 (source point clamped to the image)
-  __device__ void px(int32_t col, int32_t row, uint32_t rgb) const {
-    const int32_t sc = col < 0 ? 0 : (col > width - 1 ? width - 1 : col);
-    const int32_t sr = row < 0 ? 0 : (row > height - 1 ? height - 1 : row);
-    write_px(out + (int64_t)(int32_t)hi2ho[sr] * out_ll + (int64_t)(int32_t)wi2wo[sc] * 2, rgb);
-  }
-};
-
 // One wave per frame.  All guide-line pixels have one colour and all circle
 // pixels another, so within each phase the write order is immaterial; only
 // "lines before circle" (WSEQ:476-494) is kept, by the barrier.
@@ -139,21 +117,7 @@ __global__ __launch_bounds__(64) void overlay_kernel(PreviewArgs a, const TrikHs
   const int f = blockIdx.x, lane = threadIdx.x;
   const Canvas cv{a.previews + (int64_t)f * a.preview_stride, a.out_ll, a.width, a.height, a.wi2wo,
                   a.hi2ho};
-  const int step = a.height / 6, hh = a.height / 2, hw = a.width / 2;  // WSEQ:471-474
-  // 8 lines x 100 offsets x 2 points: drawRgbTargetCenterLine (vertical,
-  // WSEQ:136-150) at 4 columns, ...HorizontalCenterLine (WSEQ:152-166) at 4 rows
-  for (int k = lane; k < 8 * 100; k += 64) {
-    const int line = k / 100, adj = k % 100, off = (line & 3) < 2 ? ((line & 3) - 2) : ((line & 3) - 1);
-    if (line < 4) {
-      const int32_t col = hw + off * step;
-      cv.px(col, hh - adj, 0xff00ff);
-      cv.px(col, hh + adj, 0xff00ff);
-    } else {
-      const int32_t row = hh + off * step;
-      cv.px(hw - adj, row, 0xff00ff);
-      cv.px(hw + adj, row, 0xff00ff);
-    }
-  }
+  draw_guides(cv, lane, 64);  // WSEQ:471-485
   __syncthreads();
   const TrikHsvTargetSums s = sums[(int64_t)f * sums_pitch];
   const uint32_t n = (uint32_t)s.points;

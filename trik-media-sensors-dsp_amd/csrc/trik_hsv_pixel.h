@@ -60,6 +60,71 @@ __device__ __forceinline__ uint32_t pixel_hsv(const PixelRgb& p, const RangeTabl
   return ((uint32_t)mx << 16) | (s << 8) | pixel_hue(p, mx, mn, t);
 }
 
+// detectHsvPixel (WSEQ:171-179) for one packed range: per-byte "outside the
+// bounds" bits compared with the expected pattern (1 for a wrapped hue).
+__device__ __forceinline__ bool detect_packed(uint32_t H, uint32_t S, uint32_t V, const PackedRange& r) {
+  const uint32_t out = ((H < (r.from & 0xFFu)) | (H > (r.to & 0xFFu))) |
+                       (((S < ((r.from >> 8) & 0xFFu)) | (S > ((r.to >> 8) & 0xFFu))) << 1) |
+                       (((V < ((r.from >> 16) & 0xFFu)) | (V > ((r.to >> 16) & 0xFFu))) << 2);
+  return out == r.expect;
+}
+
+// H, S, V bytes (WSEQ:207-249) with LUT43 / LUT255 from any address space.
+template <typename L>
+__device__ __forceinline__ void pixel_hsv_bytes(const PixelRgb& p, const L* l43, const L* l255, uint32_t& H,
+                                                uint32_t& S, uint32_t& V) {
+  const int mx = max(p.r, max(p.g, p.b)), mn = min(p.r, min(p.g, p.b));
+  const int m = l43[mx - mn];
+  int h;
+  if (mx == p.g) h = 21845 + m * (p.b - p.r);
+  else if (mx == p.b) h = 43690 + m * (p.r - p.g);
+  else h = m * (p.g - p.b);
+  H = ((uint32_t)h >> 8) & 0xFFu;
+  S = ((uint32_t)l255[mx] * (uint32_t)(mx - mn)) >> 8;
+  V = (uint32_t)mx;
+}
+
+// writeOutputPixel, WSEQ:66-70: 0x00RRGGBB -> B5 G6 R5 (R in the low bits),
+// little-endian bytes (the output line length need not be even).
+__device__ __forceinline__ void write_px565(uint8_t* dst, uint32_t rgb888) {
+  const uint32_t v = ((rgb888 >> 19) & 0x001fu) | ((rgb888 >> 5) & 0x07e0u) | ((rgb888 << 8) & 0xf800u);
+  dst[0] = (uint8_t)v;
+  dst[1] = (uint8_t)(v >> 8);
+}
+
+// drawOutputPixelBound (WSEQ:72-89, OSEQ:77-90): the source point clamped to
+// the image, then through the scale maps.
+struct Canvas {
+  uint8_t* out;
+  int out_ll, width, height;
+  const uint32_t* wi2wo;
+  const uint32_t* hi2ho;
+  __device__ void px(int32_t col, int32_t row, uint32_t rgb) const {
+    const int32_t sc = col < 0 ? 0 : (col > width - 1 ? width - 1 : col);
+    const int32_t sr = row < 0 ? 0 : (row > height - 1 ? height - 1 : row);
+    write_px565(out + (int64_t)(int32_t)hi2ho[sr] * out_ll + (int64_t)(int32_t)wi2wo[sc] * 2, rgb);
+  }
+};
+
+// The 8 magenta guide lines of the object sensors (WSEQ:136-166,471-485;
+// OSEQ:227-255,548-561): 4 vertical and 4 horizontal lines of 2 x 100 points
+// around the centre, step = H/6; one colour, so any lane order.
+__device__ __forceinline__ void draw_guides(const Canvas& cv, int lane, int nlanes) {
+  const int step = cv.height / 6, hh = cv.height / 2, hw = cv.width / 2;
+  for (int k = lane; k < 8 * 100; k += nlanes) {
+    const int line = k / 100, adj = k % 100, off = (line & 3) < 2 ? ((line & 3) - 2) : ((line & 3) - 1);
+    if (line < 4) {
+      const int32_t col = hw + off * step;
+      cv.px(col, hh - adj, 0xff00ff);
+      cv.px(col, hh + adj, 0xff00ff);
+    } else {
+      const int32_t row = hh + off * step;
+      cv.px(hw - adj, row, 0xff00ff);
+      cv.px(hw + adj, row, 0xff00ff);
+    }
+  }
+}
+
 // (Y, U, V) of pixel `col` of row `row`: packed YUYV (WSEQ:262-270) or the
 // ov7670 planes (OSEQ:360-373: U = odd chroma byte, V = even chroma byte).
 __device__ __forceinline__ void fetch_yuv(const uint8_t* frame, int height, int line_length, int layout,

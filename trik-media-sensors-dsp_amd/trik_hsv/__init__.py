@@ -162,6 +162,50 @@ class Detector:
         return previews
 
 
+    def blob_batch(self, frames, width, height, line_length, hsv, *, n_frames=None, frame_stride=None,
+                   meta=False, labels=False, stream=None):
+        """The ov7670 multi-blob sensor over N frames (OSEQ:516-602) for the range
+        hsv = (hue, hueTol, sat, satTol, val, valTol).  Returns a dict of device
+        tensors: targets int8 [N, 8, 4] (x, y, size, 0), top int32 [N, 8, 3]
+        (size, sum_x, sum_y), n_labels int32 [N], and meta uint8 / labels int16
+        [N, H/4, W/4] when asked (else meta is the handle's scratch, None here)."""
+        import torch
+
+        b = _batch(frames, width, height, line_length, LAYOUT_OV7670, n_frames, frame_stride)
+        dev = frames.device
+        out = {"targets": torch.empty((b.n_frames, 8, 4), dtype=torch.int8, device=dev),
+               "top": torch.empty((b.n_frames, 8, 3), dtype=torch.int32, device=dev),
+               "n_labels": torch.empty((b.n_frames,), dtype=torch.int32, device=dev),
+               "meta": torch.empty((b.n_frames, height // 4, width // 4), dtype=torch.uint8, device=dev)
+               if meta else None,
+               "labels": torch.empty((b.n_frames, height // 4, width // 4), dtype=torch.int16, device=dev)
+               if labels else None}
+        ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        alg = _abi.OV7670InArgsAlg(1, *[int(v) for v in hsv], 0)
+        rc = _lib.trik_hsv_blob_batch(self._h, C.byref(b), C.byref(alg), ptr(out["targets"]), ptr(out["top"]),
+                                      ptr(out["meta"]), ptr(out["labels"]), ptr(out["n_labels"]),
+                                      _stream_ptr(stream))
+        if rc:
+            raise TrikHsvError(rc, "trik_hsv_blob_batch")
+        return out
+
+    def blob_preview(self, frames, width, height, line_length, meta, top, *, out_width=None,
+                     out_height=None, out_line_length=None, n_frames=None, frame_stride=None, stream=None):
+        """Multi-blob previews (uint8 [N, out_height, out_line_length]) from blob_batch's meta and top."""
+        import torch
+
+        b = _batch(frames, width, height, line_length, LAYOUT_OV7670, n_frames, frame_stride)
+        ow = width // 2 if out_width is None else out_width
+        oh = height // 2 if out_height is None else out_height
+        oll = 2 * ow if out_line_length is None else out_line_length
+        previews = torch.empty((b.n_frames, oh, oll), dtype=torch.uint8, device=frames.device)
+        rc = _lib.trik_hsv_blob_preview(self._h, C.byref(b), C.c_void_p(meta.data_ptr()),
+                                        C.c_void_p(top.data_ptr()), ow, oh, oll,
+                                        C.c_void_p(previews.data_ptr()), oh * oll, _stream_ptr(stream))
+        if rc:
+            raise TrikHsvError(rc, "trik_hsv_blob_preview")
+        return previews
+
     def line_preview(self, frames, width, height, line_length, val_from, val_to, sums, *,
                      out_width=None, out_height=None, out_line_length=None, n_frames=None,
                      frame_stride=None, stream=None):
@@ -339,6 +383,24 @@ class ObjectSensor:
                                                C.byref(oa))
         return rc, oa
 
+    def _bufs(self, frame, out_buffer, num_bytes):
+        import numpy as np
+
+        fr = np.ascontiguousarray(np.frombuffer(frame, np.uint8) if isinstance(frame, (bytes, bytearray))
+                                  else frame, dtype=np.uint8)
+        ib = _abi.BufDesc1()
+        ib.numBufs = 1
+        ib.descs[0].buf = fr.ctypes.data
+        ib.descs[0].bufSize = fr.size
+        ob = _abi.BufDesc()
+        keep = [fr]
+        if out_buffer is not None:
+            ob_arr = (C.c_void_p * 1)(out_buffer.ctypes.data)
+            sz_arr = (C.c_int32 * 1)(out_buffer.nbytes)
+            keep += [ob_arr, sz_arr]
+            ob.bufs, ob.numBufs, ob.bufSizes = ob_arr, 1, sz_arr
+        return fr, ib, ob, keep
+
 
 class LineSensor(ObjectSensor):
     """The ov7670 line sensor's codec instance (trik/ov7670/line_sensor glue,
@@ -352,3 +414,31 @@ class LineSensor(ObjectSensor):
         super().__init__(params)
         if params is None:
             self.params = _default_params(1, fmt_in=FORMAT_YUV422P)
+
+
+class BlobSensor(ObjectSensor):
+    """The ov7670 object sensor's codec instance (trik/ov7670/object_sensor:
+    BallDetector<YUV422P, RGB565X> with BitmapBuilder + Clusterizer): its own
+    InArgs (centre/tolerance, sticky via setHsvRange) and OutArgs (target[8])."""
+
+    _create = "TRIK_VIDTRANSCODE_CV_create_ov7670"
+
+    def __init__(self, params: _abi.Params | None = None):
+        super().__init__(params)
+        if params is None:
+            self.params = _default_params(1, fmt_in=FORMAT_YUV422P)
+
+    def process(self, frame, hsv=None, out_buffer=None, auto_detect=False, num_bytes=None, input_id=0):
+        """One host frame -> (rc, OV7670OutArgs).  hsv = (hue, hueTol, sat,
+        satTol, val, valTol) sets the range (setHsvRange); None keeps it."""
+        fr, ib, ob, keep = self._bufs(frame, out_buffer, num_bytes)
+        ia = _abi.OV7670InArgs()
+        ia.base.size = C.sizeof(_abi.OV7670InArgs)
+        ia.base.numBytes = fr.size if num_bytes is None else num_bytes
+        ia.base.inputID = input_id
+        vals = [int(v) for v in hsv] if hsv is not None else [0] * 6
+        ia.alg = _abi.OV7670InArgsAlg(1 if hsv is not None else 0, *vals, int(bool(auto_detect)))
+        oa = _abi.OV7670OutArgs()
+        oa.base.size = C.sizeof(_abi.OV7670OutArgs)
+        rc = _lib.TRIK_VIDTRANSCODE_CV_process(self._h, C.byref(ib), C.byref(ob), C.byref(ia), C.byref(oa))
+        return rc, oa

@@ -83,11 +83,29 @@ class InArgs(C.Structure):
     _fields_ = [("base", IVidtranscodeInArgs), ("alg", InArgsAlg)]
 
 
+
 class OutArgsAlg(C.Structure):
     """TRIK_VIDTRANSCODE_CV_OutArgsAlg (webcam trik_vidtranscode_cv.h:64-74)."""
     _fields_ = [("targetX", C.c_int8), ("targetY", C.c_int8), ("targetSize", u8),
                 ("detectHue", u16), ("detectHueTolerance", u16), ("detectSat", u16),
                 ("detectSatTolerance", u16), ("detectVal", u16), ("detectValTolerance", u16)]
+
+
+class OV7670InArgsAlg(C.Structure):
+    """TRIK_VIDTRANSCODE_CV_OV7670_InArgsAlg (ov7670 object sensor trik_vidtranscode_cv.h:51-60)."""
+    _fields_ = [("setHsvRange", i32), ("detectHue", u16), ("detectHueTol", u16), ("detectSat", u8),
+                ("detectSatTol", u8), ("detectVal", u8), ("detectValTol", u8), ("autoDetectHsv", i32)]
+
+
+class XdasTarget(C.Structure):
+    _fields_ = [("x", C.c_int8), ("y", C.c_int8), ("size", u8)]
+
+
+class OV7670OutArgsAlg(C.Structure):
+    """TRIK_VIDTRANSCODE_CV_OV7670_OutArgsAlg (ov7670 trik_vidtranscode_cv.h:73-81)."""
+    _fields_ = [("target", XdasTarget * 8), ("detectHue", u16), ("detectHueTolerance", u16),
+                ("detectSat", u16), ("detectSatTolerance", u16), ("detectVal", u16),
+                ("detectValTolerance", u16)]
 
 
 class SingleBufDesc(C.Structure):
@@ -113,6 +131,14 @@ class IVidtranscodeOutArgs(C.Structure):
 
 class OutArgs(C.Structure):
     _fields_ = [("base", IVidtranscodeOutArgs), ("alg", OutArgsAlg)]
+
+
+class OV7670InArgs(C.Structure):
+    _fields_ = [("base", IVidtranscodeInArgs), ("alg", OV7670InArgsAlg)]
+
+
+class OV7670OutArgs(C.Structure):
+    _fields_ = [("base", IVidtranscodeOutArgs), ("alg", OV7670OutArgsAlg)]
 
 
 class AlgBufInfo(C.Structure):
@@ -142,9 +168,12 @@ class Target(C.Structure):
 PROTOTYPES = {
     "TRIK_VIDTRANSCODE_CV_create": ([C.POINTER(Params), C.POINTER(C.c_void_p)], i32),
     "TRIK_VIDTRANSCODE_CV_create_line": ([C.POINTER(Params), C.POINTER(C.c_void_p)], i32),
+    "TRIK_VIDTRANSCODE_CV_create_ov7670": ([C.POINTER(Params), C.POINTER(C.c_void_p)], i32),
     "TRIK_VIDTRANSCODE_CV_delete": ([C.c_void_p], i32),
+    # InArgs / OutArgs by pointer: the webcam structs, or the OV7670 ones for
+    # a create_ov7670 handle (their base.size fields say which)
     "TRIK_VIDTRANSCODE_CV_process": ([C.c_void_p, C.POINTER(BufDesc1), C.POINTER(BufDesc),
-                                      C.POINTER(InArgs), C.POINTER(OutArgs)], i32),
+                                      C.c_void_p, C.c_void_p], i32),
     "TRIK_VIDTRANSCODE_CV_control": ([C.c_void_p, i32, C.POINTER(DynamicParams),
                                       C.POINTER(Status)], i32),
     "trik_hsv_version": ([], C.c_char_p),
@@ -163,6 +192,10 @@ PROTOTYPES = {
     "trik_hsv_line_batch": ([C.POINTER(FrameBatch), i32, i32, i32, i32, C.c_void_p, C.c_void_p,
                              C.c_void_p], i32),
     "trik_hsv_line_preview": ([C.c_void_p, C.POINTER(FrameBatch), i32, i32, C.c_void_p, i32, i32, i32,
+                               C.c_void_p, C.c_int64, C.c_void_p], i32),
+    "trik_hsv_blob_batch": ([C.c_void_p, C.POINTER(FrameBatch), C.POINTER(OV7670InArgsAlg), C.c_void_p,
+                             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], i32),
+    "trik_hsv_blob_preview": ([C.c_void_p, C.POINTER(FrameBatch), C.c_void_p, C.c_void_p, i32, i32, i32,
                                C.c_void_p, C.c_int64, C.c_void_p], i32),
     "trik_hsv_synth": ([C.POINTER(FrameBatch), i32, i32, u64, C.c_void_p], i32),
 }
