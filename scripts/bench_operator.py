@@ -9,6 +9,8 @@
   line        trik_hsv_line_batch: 4096 x 640x480 ov7670 (YUV422P) frames, the
               line sensor's sums + OutArgs; algorithmic bytes = both planes
               (2 B/px) once.  line_preview: its 320x240 previews.
+  blob        trik_hsv_blob_batch: 4096 x 640x480 ov7670 frames through the
+              multi-blob sensor (metapixel bitmap + clusterer + 8 targets).
   process     one host frame through the XDAIS quartet (H2D + kernels + D2H,
               PCIe-inclusive latency per frame), with preview and auto range.
 
@@ -95,6 +97,12 @@ def main():
     out["line_preview"] = {"frames": lf, "ms": round(lp_ms, 4),
                            "achieved_GBs": round(lp_bytes / (lp_ms / 1e3) / 1e9, 1),
                            "hbm_frac": round(lp_bytes / (lp_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+    RED = (0, 20, 80, 20, 50, 50)
+    bl_ms = timed(lambda: det.blob_batch(ldev, W, H, W, RED), stream, args.iters)
+    out["blob"] = {"frames": lf, "ms": round(bl_ms, 4), "Mframes_per_s": round(lf / bl_ms / 1e3, 3),
+                   "achieved_GBs": round(lf * lfb / (bl_ms / 1e3) / 1e9, 1),
+                   "hbm_frac": round(lf * lfb / (bl_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                   "note": "blob_meta_kernel + blob_ccl_kernel (one wave per frame)"}
     del ldev
 
     s = trik_hsv.ObjectSensor()

@@ -117,9 +117,18 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
   uint16_t* cur = prev + bw;                    // [bw] labels of row r
   uint16_t* up = cur + bw;                      // [bw] up-row minimum, kInf if none
   uint8_t* dset = reinterpret_cast<uint8_t*>(up + bw);  // [bw] set flags of row r
+  // the frame's bitmap: staged in LDS when it fits (bw*bh is a multiple of 8)
   const uint8_t* meta = a.meta + (int64_t)f * bw * bh;
-  int32_t* own = a.stats + (int64_t)f * 2 * 3 * ml;  // own[3k + {0,1,2}] = x, y, size
-  int32_t* fin = own + 3 * ml;
+  if (a.meta_lds) {
+    uint32_t* dst = reinterpret_cast<uint32_t*>(dset + bw);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(meta);
+    for (int i = lane; i < bw * bh / 4; i += 64) dst[i] = src[i];
+    meta = dset + bw;
+    __syncthreads();
+  }
+  // own[3k + {0,1,2}] = x, y, size (zeroed by the launcher); fin: folded
+  int32_t* own = a.stats + (int64_t)f * 3 * ml;
+  int32_t* fin = a.stats + ((int64_t)a.n_frames + f) * 3 * ml;
   uint16_t* labels = a.labels ? a.labels + (int64_t)f * bw * bh : nullptr;
 
   const int K = (bw + 63) / 64;  // columns per lane, contiguous
@@ -193,9 +202,6 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
         }
         if (!left && up[c] == kInf) {  // CLU:98-112
           eq[lbl] = (uint16_t)lbl;
-          own[3 * lbl] = 0;
-          own[3 * lbl + 1] = 0;
-          own[3 * lbl + 2] = 0;
           run = lbl++;
         } else {
           run = min(run, (uint32_t)up[c]);
@@ -204,8 +210,6 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
       }
     }
     next += (int)total;
-    __threadfence_block();
-    __threadfence();
     __syncthreads();
     // phase 4: statistics of the non-opening metapixels, one atomic per run of
     // equal labels; equivalence events flagged
@@ -354,14 +358,20 @@ int launch_blob(const BlobArgs& a, hipStream_t s) {
   if (a.n_frames <= 0 || a.width <= 0 || a.height <= 0) return hipSuccess;
   const int bw = a.width >> 2, bh = a.height >> 2;
   if (bw > 64 * 32) return hipErrorInvalidValue;  // events mask: 32 columns per lane
+  // own statistics start at zero ([n][max_labels][3] at the front of stats)
+  hipError_t z = hipMemsetAsync(a.stats, 0, sizeof(int32_t) * 3 * (size_t)a.max_labels * (size_t)a.n_frames, s);
+  if (z != hipSuccess) return z;
   const int64_t mblocks = (int64_t)a.n_frames * bh * ((bw + kMetaCols - 1) / kMetaCols);
   if (mblocks > 0x7FFFFFFF) return hipErrorInvalidValue;
   hipLaunchKernelGGL(blob_meta_kernel, dim3((unsigned)mblocks), dim3(256), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const size_t lds = sizeof(uint16_t) * ((size_t)((a.max_labels + 1) & ~1) + 3 * (size_t)bw) + (size_t)bw;
+  size_t lds = sizeof(uint16_t) * ((size_t)((a.max_labels + 1) & ~1) + 3 * (size_t)bw) + (size_t)bw;
   if (lds > 64 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(blob_ccl_kernel, dim3((unsigned)a.n_frames), dim3(64), lds, s, a);
+  BlobArgs b = a;
+  b.meta_lds = lds + (size_t)bw * bh <= 40 * 1024 ? 1 : 0;  // keep ~4 frames per CU resident
+  if (b.meta_lds) lds += (size_t)bw * bh;
+  hipLaunchKernelGGL(blob_ccl_kernel, dim3((unsigned)a.n_frames), dim3(64), lds, s, b);
   return hipGetLastError();
 }
 
