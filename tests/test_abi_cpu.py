@@ -32,7 +32,10 @@ def test_header_declares_the_quartet_and_batch_api():
     for n in ("TRIK_VIDTRANSCODE_CV_create", "TRIK_VIDTRANSCODE_CV_delete",
               "TRIK_VIDTRANSCODE_CV_process", "TRIK_VIDTRANSCODE_CV_control",
               "trik_hsv_process_batch", "trik_hsv_batch_sums", "trik_hsv_batch_targets",
-              "trik_hsv_batch_masks", "trik_hsv_synth", "trik_hsv_version", "trik_hsv_last_error"):
+              "trik_hsv_batch_masks", "trik_hsv_synth", "trik_hsv_version", "trik_hsv_last_error",
+              "TRIK_VIDTRANSCODE_CV_create_line", "TRIK_VIDTRANSCODE_CV_create_ov7670",
+              "trik_hsv_line_batch", "trik_hsv_line_preview", "trik_hsv_blob_batch", "trik_hsv_blob_preview",
+              "trik_hsv_batch_preview", "trik_hsv_batch_auto_range"):
         assert n in names
 
 
@@ -52,17 +55,22 @@ STRUCTS = ["TRIK_VIDTRANSCODE_CV_Params", "TRIK_VIDTRANSCODE_CV_DynamicParams",
            "TRIK_VIDTRANSCODE_CV_InArgsAlg", "TRIK_VIDTRANSCODE_CV_InArgs",
            "TRIK_VIDTRANSCODE_CV_OutArgsAlg", "TRIK_VIDTRANSCODE_CV_OutArgs",
            "TRIK_XDM1_BufDesc", "TRIK_XDM_BufDesc", "TRIK_IVIDTRANSCODE_Status",
-           "TrikHsvFrameBatch", "TrikHsvTargetSums", "TrikHsvTarget"]
+           "TrikHsvFrameBatch", "TrikHsvTargetSums", "TrikHsvTarget",
+           "TRIK_VIDTRANSCODE_CV_OV7670_InArgsAlg", "TRIK_VIDTRANSCODE_CV_OV7670_InArgs",
+           "TRIK_XDAS_Target", "TRIK_VIDTRANSCODE_CV_OV7670_OutArgsAlg", "TRIK_VIDTRANSCODE_CV_OV7670_OutArgs"]
 MIRRORS = ["Params", "DynamicParams", "InArgsAlg", "InArgs", "OutArgsAlg", "OutArgs",
-           "BufDesc1", "BufDesc", "Status", "FrameBatch", "TargetSums", "Target"]
+           "BufDesc1", "BufDesc", "Status", "FrameBatch", "TargetSums", "Target",
+           "OV7670InArgsAlg", "OV7670InArgs", "XdasTarget", "OV7670OutArgsAlg", "OV7670OutArgs"]
 
 
 def test_struct_layout_matches_c(abi):
     prog = "#include <stdio.h>\n#include \"trik_hsv.h\"\nint main(void){\n"
     for s in STRUCTS:
         prog += f'  printf("%zu\\n", sizeof({s}));\n'
-    prog += '  printf("%zu %zu\\n", offsetof(TRIK_VIDTRANSCODE_CV_OutArgs, alg), ' \
-            'offsetof(TRIK_VIDTRANSCODE_CV_InArgs, alg));\n  return 0;\n}\n'
+    prog += '  printf("%zu %zu %zu %zu\\n", offsetof(TRIK_VIDTRANSCODE_CV_OV7670_OutArgs, alg), ' \
+            'offsetof(TRIK_VIDTRANSCODE_CV_OV7670_InArgs, alg), ' \
+            'offsetof(TRIK_VIDTRANSCODE_CV_OutArgs, alg), offsetof(TRIK_VIDTRANSCODE_CV_InArgs, alg));\n' \
+            '  return 0;\n}\n'
     with tempfile.TemporaryDirectory() as d:
         c = os.path.join(d, "sz.c")
         open(c, "w").write(prog.replace("#include <stdio.h>", "#include <stdio.h>\n#include <stddef.h>"))
@@ -73,6 +81,7 @@ def test_struct_layout_matches_c(abi):
     for s, m, n in zip(STRUCTS, MIRRORS, sizes):
         assert C.sizeof(getattr(abi, m)) == n, (s, C.sizeof(getattr(abi, m)), n)
     assert int(out[-2]) == abi.OutArgs.alg.offset and int(out[-1]) == abi.InArgs.alg.offset
+    assert int(out[-4]) == abi.OV7670OutArgs.alg.offset and int(out[-3]) == abi.OV7670InArgs.alg.offset
 
 
 def test_header_compiles_as_cxx():
