@@ -47,6 +47,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=4096)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the oracle CPU baselines")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -103,6 +104,7 @@ def main():
                    "achieved_GBs": round(lf * lfb / (bl_ms / 1e3) / 1e9, 1),
                    "hbm_frac": round(lf * lfb / (bl_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                    "note": "blob_meta_kernel + blob_ccl_kernel (one wave per frame)"}
+    ldev_host = ldev[: 8 * lfb].cpu().numpy()
     del ldev
 
     s = trik_hsv.ObjectSensor()
@@ -122,7 +124,49 @@ def main():
                                            "PCIe-inclusive, one synchronous call per frame"}
     s.close()
     det.close()
+    if not args.no_cpu:
+        cpu_baselines(out, dev, ldev_host, W, H, LL, OW, OH, OLL, T0)
     print(json.dumps(out))
+
+
+def cpu_baselines(out, dev, ldev_host, W, H, LL, OW, OH, OLL, T0):
+    """The oracle (C restatement of the reference, one thread) on a few of the
+    same frames, per row: ms per frame, beside the GPU's ms per frame."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    oracle.build()
+    n = 8
+    fb = H * LL
+    frames = dev[: n * fb].cpu().numpy()
+    lfb = 2 * H * W
+    lframes = ldev_host[: n * lfb]
+
+    def per_frame(fn):
+        t0 = time.perf_counter()
+        for i in range(n):
+            fn(i)
+        return (time.perf_counter() - t0) / n * 1e3
+
+    rows = {
+        "preview": lambda i: oracle.run(frames[i * fb:(i + 1) * fb], W, H, LL, 0, T0, out_width=OW,
+                                        out_height=OH, out_line_length=OLL),
+        "auto_range": lambda i: oracle.run(frames[i * fb:(i + 1) * fb], W, H, LL, 0, T0, auto_detect=True,
+                                           preview=False),
+        "line": lambda i: oracle.line_run(lframes[i * lfb:(i + 1) * lfb], W, H, W, 0, 30, preview=False),
+        "blob": lambda i: oracle.blob_run(lframes[i * lfb:(i + 1) * lfb], W, H, W, hsv=(0, 20, 80, 20, 50, 50),
+                                          preview=False),
+    }
+    for k, fn in rows.items():
+        ms = per_frame(fn)
+        gpu_ms = out[k]["ms"] / out[k]["frames"]
+        out[k]["cpu_baseline"] = {"kind": "port", "cores": 1, "ms_per_frame": round(ms, 3),
+                                  "sample": f"{n} frames of the same batch, oracle (whole run incl. its "
+                                            "per-pixel HSV pass), single thread",
+                                  "gpu_ms_per_frame": round(gpu_ms, 6),
+                                  "gpu_over_cpu": round(ms / gpu_ms, 1)}
 
 
 if __name__ == "__main__":

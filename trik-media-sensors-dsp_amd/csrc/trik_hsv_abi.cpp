@@ -168,7 +168,7 @@ struct TrikCvHandle {
 
   // ov7670 multi-blob sensor: BitmapBuilder's sticky range (uninitialised in
   // the reference before the first setHsvRange; zero here) and scratch
-  PackedRange blob_range{0u, 0u, 0u};
+  TRIK_VIDTRANSCODE_CV_InArgsAlg blob_range{};  // as webcam-form bounds (all zero at first)
   uint8_t* d_meta = nullptr;
   size_t d_meta_cap = 0;
   int32_t* d_blob_stats = nullptr;
@@ -431,7 +431,7 @@ int clip_value(int v, int adj, int lo, int hi) {  // makeValueRange, stdcpp.hpp
   v += adj;
   return v > hi ? hi : (v < lo ? lo : v);
 }
-PackedRange blob_pack(const TRIK_VIDTRANSCODE_CV_OV7670_InArgsAlg& a) {
+TRIK_VIDTRANSCODE_CV_InArgsAlg blob_range_args(const TRIK_VIDTRANSCODE_CV_OV7670_InArgsAlg& a) {
   TRIK_VIDTRANSCODE_CV_InArgsAlg r;
   memset(&r, 0, sizeof r);
   r.detectHueFrom = (uint16_t)wrap_value(a.detectHue, -(int)a.detectHueTol, 0, 359);
@@ -440,7 +440,7 @@ PackedRange blob_pack(const TRIK_VIDTRANSCODE_CV_OV7670_InArgsAlg& a) {
   r.detectSatTo = (uint8_t)clip_value(a.detectSat, (int)a.detectSatTol, 0, 100);
   r.detectValFrom = (uint8_t)clip_value(a.detectVal, -(int)a.detectValTol, 0, 100);
   r.detectValTo = (uint8_t)clip_value(a.detectVal, (int)a.detectValTol, 0, 100);
-  return pack_range(r);  // same scaling and wrap packing (WSEQ:425-445 = BMB:62-77)
+  return r;  // then the same scaling and wrap packing (WSEQ:425-445 = BMB:62-77)
 }
 
 template <typename T>
@@ -466,14 +466,18 @@ int32_t ensure_blob_scratch(TrikCvHandle* h, int n, int w, int hgt) {
   return r;
 }
 
-BlobArgs blob_args(TrikCvHandle* h, const TrikHsvFrameBatch& b, PackedRange range, TrikHsvTarget* targets,
-                   int32_t* top, uint8_t* meta, uint16_t* labels, int32_t* n_labels) {
-  BlobArgs a;
+// Compiles the range's tables (cached per handle) and fills the kernel args.
+int32_t blob_args(TrikCvHandle* h, const TrikHsvFrameBatch& b, const TRIK_VIDTRANSCODE_CV_InArgsAlg& range,
+                  TrikHsvTarget* targets, int32_t* top, uint8_t* meta, uint16_t* labels, int32_t* n_labels,
+                  hipStream_t s, BlobArgs& a) {
+  int32_t rc = ensure_tables(h, &range, 1, s);
+  if (rc) return rc;
   a.frames = static_cast<const uint8_t*>(b.frames);
   a.frame_stride = b.frame_stride;
   a.n_frames = b.n_frames;
   a.width = b.width; a.height = b.height; a.line_length = b.line_length;
-  a.range = range;
+  a.range = pack_range(range);
+  a.tables = h->d_stripe;
   a.aligned4 = (reinterpret_cast<uintptr_t>(b.frames) & 3) == 0 && (b.n_frames <= 1 || (b.frame_stride & 3) == 0) &&
                (b.line_length & 3) == 0;
   a.meta = meta ? meta : h->d_meta;
@@ -483,7 +487,7 @@ BlobArgs blob_args(TrikCvHandle* h, const TrikHsvFrameBatch& b, PackedRange rang
   a.targets = targets ? targets : h->d_blob_targets;
   a.top = top ? top : h->d_blob_top;
   a.n_labels = n_labels;
-  return a;
+  return 0;
 }
 
 AutoRangeArgs auto_range_args(const TrikHsvFrameBatch& b, uint16_t* out) {
@@ -680,10 +684,12 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
         TrikHsvFrameBatch b = {h->d_frame, (int64_t)fb, 1, h->in_w, h->in_h, h->in_ll, h->layout};
         HIP_TRY(hipMemsetAsync(h->d_sums, 0, sizeof(TrikHsvTargetSums), h->stream));
         if (blob) {  // BallDetector<YUV422P>::run, OSEQ:516-602
-          if (ia7->alg.setHsvRange) h->blob_range = blob_pack(ia7->alg);  // BMB:110-130
+          if (ia7->alg.setHsvRange) h->blob_range = blob_range_args(ia7->alg);  // BMB:110-130
           int32_t r = ensure_blob_scratch(h, 1, h->in_w, h->in_h);
           if (r) return r;
-          const BlobArgs ba = blob_args(h, b, h->blob_range, nullptr, nullptr, nullptr, nullptr, nullptr);
+          BlobArgs ba;
+          r = blob_args(h, b, h->blob_range, nullptr, nullptr, nullptr, nullptr, nullptr, h->stream, ba);
+          if (r) return r;
           HIP_TRY(launch_blob(ba, h->stream));
           if (out_ptr && out_size > 0) {  // preview: set metapixels, guide lines, target marks
             const size_t pb = (size_t)out_size;
@@ -979,8 +985,12 @@ extern "C" int32_t trik_hsv_blob_batch(TRIK_VIDTRANSCODE_CV_Handle h, const Trik
   }
   int32_t r = ensure_blob_scratch(h, b->n_frames, b->width, b->height);
   if (r) return r;
-  const BlobArgs ba = blob_args(h, *b, blob_pack(*hsv), targets, top, meta, labels, n_labels);
+  BlobArgs ba;
+  r = blob_args(h, *b, blob_range_args(*hsv), targets, top, meta, labels, n_labels, s, ba);
+  if (r) return r;
   HIP_TRY(launch_blob(ba, s));
+  if (!h->tables_busy) HIP_TRY(hipEventCreateWithFlags(&h->tables_busy, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(h->tables_busy, s));
   if (!h->blob_busy) HIP_TRY(hipEventCreateWithFlags(&h->blob_busy, hipEventDisableTiming));
   HIP_TRY(hipEventRecord(h->blob_busy, s));
   return 0;

@@ -33,54 +33,93 @@
 
 #include "trik_hsv_internal.h"
 #include "trik_hsv_pixel.h"
+#include "trik_hsv_stripe_px.h"
 
 namespace trik_hsv {
 
 namespace {
 
-constexpr int kMetaCols = 64;  // metapixel columns per 256-lane workgroup
+using namespace stripe_px;
 
-__global__ __launch_bounds__(256) void blob_meta_kernel(BlobArgs a) {
-  __shared__ uint16_t l43[256], l255[256];
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) {  // OSEQ:489-499
-    l43[i] = i ? (uint16_t)((43u * 256u) / (uint32_t)i) : 0;
-    l255[i] = i ? (uint16_t)((255u * 256u) / (uint32_t)i) : 0;
+// x / d for 32-bit x via a host-computed multiplier (round-up method):
+// q = (umulhi(x, magic) + x) >> shift, exact for every 32-bit x.
+struct FastDiv {
+  uint32_t magic, shift, d;
+};
+inline FastDiv make_div(uint32_t d) {
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  const uint64_t m = ((1ull << 32) * ((1ull << s) - d)) / d + 1;
+  return FastDiv{(uint32_t)m, s, d};
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
+  return (uint32_t)(((uint64_t)__umulhi(x, f.magic) + x) >> f.shift);
+}
+
+struct MetaGeom {
+  FastDiv per_frame;  // bw * bh
+  FastDiv per_row;    // bw
+  uint32_t total;     // n_frames * bw * bh
+};
+
+// The metapixel flags with the hot kernel's per-pixel arithmetic and its
+// StripeTables image (range 0 = the sticky range) staged at LDS address 0:
+// four lanes per metapixel (one per pixel row of it, 4 pixels each), 256
+// metapixels per 1024-lane workgroup per iteration, grid-stride over all
+// metapixels of the batch; two workgroups per CU as stripe_kernel.
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8)))
+void blob_meta_kernel(BlobArgs a, MetaGeom g) {
+  {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4* src = reinterpret_cast<const u32x4*>(a.tables);
+    typedef __attribute__((address_space(3))) u32x4* lds_u128_wptr;
+    lds_u128_wptr dst = (lds_u128_wptr)(uintptr_t)0;
+    for (int i = threadIdx.x; i < (int)(sizeof(StripeTables) / 16); i += blockDim.x) dst[i] = src[i];
   }
   __syncthreads();
-  const int bw = a.width >> 2, bh = a.height >> 2;
-  const int chunks = (bw + kMetaCols - 1) / kMetaCols;
-  const int per_frame = bh * chunks;
-  const int f = blockIdx.x / per_frame;
-  const int rem = blockIdx.x - f * per_frame;
-  const int mr = rem / chunks;
-  const int mc = (rem - mr * chunks) * kMetaCols + (threadIdx.x >> 2);
-  const int rr = threadIdx.x & 3;
-  uint32_t cnt = 0;
-  if (mc < bw) {
-    const int64_t ll = a.line_length;
-    const uint8_t* yp = a.frames + (int64_t)f * a.frame_stride + (int64_t)(4 * mr + rr) * ll + 4 * mc;
-    const uint8_t* cp = yp + (int64_t)a.height * ll;
-    uint32_t yw, cw;
-    if (a.aligned4) {
-      yw = *reinterpret_cast<const uint32_t*>(yp);
-      cw = *reinterpret_cast<const uint32_t*>(cp);
-    } else {
-      yw = (uint32_t)yp[0] | ((uint32_t)yp[1] << 8) | ((uint32_t)yp[2] << 16) | ((uint32_t)yp[3] << 24);
-      cw = (uint32_t)cp[0] | ((uint32_t)cp[1] << 8) | ((uint32_t)cp[2] << 16) | ((uint32_t)cp[3] << 24);
-    }
+  const int t = threadIdx.x;
+  const uint32_t hue_lane = (uint32_t)offsetof(StripeTables, hue) + ((t % kHueCopies) << 2);
+  const uint32_t m43_lane = (uint32_t)offsetof(StripeTables, m43) + ((t % kM43Copies) << 2);
+  const int rr = t & 3;
+  const uint32_t bw = g.per_row.d;
+  const int64_t ll = a.line_length;
+  for (uint32_t base = blockIdx.x * 256u; base < g.total; base += gridDim.x * 256u) {
+    const uint32_t m = base + (uint32_t)(t >> 2);
+    const bool valid = m < g.total;
+    uint32_t cnt = 0;
+    if (valid) {
+      const uint32_t f = fdiv(m, g.per_frame), rem = m - f * g.per_frame.d;
+      const uint32_t mr = fdiv(rem, g.per_row), mc = rem - mr * bw;
+      const uint8_t* yp = a.frames + (int64_t)f * a.frame_stride + (int64_t)(4 * mr + rr) * ll + 4 * mc;
+      const uint8_t* cp = yp + (int64_t)a.height * ll;
+      uint32_t yy, cc;
+      if (a.aligned4) {
+        yy = *reinterpret_cast<const uint32_t*>(yp);
+        cc = *reinterpret_cast<const uint32_t*>(cp);
+      } else {
+        yy = (uint32_t)yp[0] | ((uint32_t)yp[1] << 8) | ((uint32_t)yp[2] << 16) | ((uint32_t)yp[3] << 24);
+        cc = (uint32_t)cp[0] | ((uint32_t)cp[1] << 8) | ((uint32_t)cp[2] << 16) | ((uint32_t)cp[3] << 24);
+      }
+      uint32_t w0, w1;
+      ov7670_words(yy, cc, w0, w1);
+      Phase1 p[4];
+      p[0] = phase1<0>(w0, w0 ^ 0xFF00FF00u, m43_lane);
+      p[1] = phase1<1>(w0, w0 ^ 0xFF00FF00u, m43_lane);
+      p[2] = phase1<0>(w1, w1 ^ 0xFF00FF00u, m43_lane);
+      p[3] = phase1<1>(w1, w1 ^ 0xFF00FF00u, m43_lane);
+      uint32_t mm[4], sv[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {  // chroma V0 U0 V1 U1: V even, U odd (OSEQ:369-373)
-      const int sh = 16 * (k >> 1);
-      const PixelRgb p = pixel_rgb((int)((yw >> (8 * k)) & 0xFFu), (int)((cw >> (sh + 8)) & 0xFFu),
-                                   (int)((cw >> sh) & 0xFFu));
-      uint32_t H, S, V;
-      pixel_hsv_bytes(p, l43, l255, H, S, V);
-      cnt += detect_packed(H, S, V, a.range) ? 1u : 0u;
+      for (int j = 0; j < 4; ++j) {
+        mm[j] = lds_u32(p[j].m43_addr);
+        sv[j] = lds_u8(p[j].sv_addr);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cnt += combine(lds_u32(phase2_addr(mm[j], p[j], hue_lane)), sv[j]) & 1u;
     }
+    cnt += __shfl_xor(cnt, 1, 64);
+    cnt += __shfl_xor(cnt, 2, 64);
+    if (rr == 0 && valid) a.meta[m] = cnt > 2 ? 1 : 0;  // (f, mr, mc) is m itself
   }
-  cnt += __shfl_xor(cnt, 1, 64);
-  cnt += __shfl_xor(cnt, 2, 64);
-  if (rr == 0 && mc < bw) a.meta[((int64_t)f * bh + mr) * bw + mc] = cnt > 2 ? 1 : 0;
 }
 
 constexpr uint32_t kInf = 0xFFFFu;
@@ -361,11 +400,33 @@ int launch_blob(const BlobArgs& a, hipStream_t s) {
   // own statistics start at zero ([n][max_labels][3] at the front of stats)
   hipError_t z = hipMemsetAsync(a.stats, 0, sizeof(int32_t) * 3 * (size_t)a.max_labels * (size_t)a.n_frames, s);
   if (z != hipSuccess) return z;
-  const int64_t mblocks = (int64_t)a.n_frames * bh * ((bw + kMetaCols - 1) / kMetaCols);
-  if (mblocks > 0x7FFFFFFF) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(blob_meta_kernel, dim3((unsigned)mblocks), dim3(256), 0, s, a);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  const int64_t total = (int64_t)a.n_frames * bw * bh;
+  if (total >= (1ll << 31) || !a.tables) return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(blob_meta_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(StripeTables));
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  if (total > 0) {
+    MetaGeom g;
+    g.per_frame = make_div((uint32_t)(bw * bh));
+    g.per_row = make_div((uint32_t)bw);
+    g.total = (uint32_t)total;
+    const int64_t chunks = (total + 255) / 256, slots = 2LL * cus;
+    hipLaunchKernelGGL(blob_meta_kernel, dim3((unsigned)(chunks < slots ? chunks : slots)), dim3(1024),
+                       sizeof(StripeTables), s, a, g);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   size_t lds = sizeof(uint16_t) * ((size_t)((a.max_labels + 1) & ~1) + 3 * (size_t)bw) + (size_t)bw;
   if (lds > 64 * 1024) return hipErrorInvalidValue;
   BlobArgs b = a;

@@ -139,6 +139,7 @@ struct BlobArgs {
   int64_t frame_stride;
   int32_t n_frames, width, height, line_length;
   PackedRange range;         // the sticky BitmapBuilder range (BMB:62-77)
+  const StripeTables* tables;  // that range compiled as range 0 (device)
   int32_t aligned4;          // frames, stride and line length 4-byte aligned
   uint8_t* meta;             // [n][H/4][W/4]: 1 for set metapixels
   uint16_t* labels;          // optional [n][H/4][W/4]: the clusterer's label map
