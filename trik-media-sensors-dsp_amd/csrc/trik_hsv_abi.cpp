@@ -126,6 +126,25 @@ std::string validate_batch(const TrikHsvFrameBatch* b) {
 // ---------------------------------------------------------------------------
 // Handle
 // ---------------------------------------------------------------------------
+// Compiled range tables (device) for one range set, with the key (packed
+// bounds) they were compiled from and their pinned staging.
+struct TableSet {
+  RangeTables* d_tables = nullptr;
+  int groups_cap = 0;
+  std::vector<uint32_t> key;
+  RangeTables* h_tables = nullptr;
+  StripeTables* d_stripe = nullptr;
+  StripeTables* h_stripe = nullptr;
+  void release() {
+    (void)hipFree(d_tables);
+    (void)hipHostFree(h_tables);
+    (void)hipFree(d_stripe);
+    (void)hipHostFree(h_stripe);
+    d_tables = nullptr; h_tables = nullptr; d_stripe = nullptr; h_stripe = nullptr;
+    groups_cap = 0;
+  }
+};
+
 struct TrikCvHandle {
   int device = 0;
   int algo = kAlgoBall;
@@ -142,12 +161,9 @@ struct TrikCvHandle {
   std::mutex mu;
 
   // compiled range tables (device) and the key they were compiled from
-  RangeTables* d_tables = nullptr;
-  int table_groups_cap = 0;
-  std::vector<uint32_t> table_key;
-  RangeTables* h_tables = nullptr;  // pinned staging
-  StripeTables* d_stripe = nullptr;
-  StripeTables* h_stripe = nullptr;
+  // two caches: the range set of the sums path, and a single range for the
+  // preview / multi-blob bitmap (so alternating calls do not recompile)
+  TableSet sums_tables, single_tables;
   hipEvent_t tables_busy = nullptr;
 
   // preview geometry: scale maps for maps_key = {W, H, out_w, out_h}
@@ -189,10 +205,8 @@ void release(TrikCvHandle* h) {
                   hipSetDevice(h->device) == hipSuccess;
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->tables_busy) (void)hipEventSynchronize(h->tables_busy);
-  (void)hipFree(h->d_tables);
-  (void)hipHostFree(h->h_tables);
-  (void)hipFree(h->d_stripe);
-  (void)hipHostFree(h->h_stripe);
+  h->sums_tables.release();
+  h->single_tables.release();
   (void)hipFree(h->d_frame);
   (void)hipFree(h->d_maps);
   (void)hipFree(h->d_preview);
@@ -268,7 +282,7 @@ int32_t setup_dynamic(TrikCvHandle* h, const TRIK_VIDTRANSCODE_CV_DynamicParams*
 }
 
 // Compile + upload the tables for ranges[0..n), stream-ordered on s.
-int32_t ensure_tables(TrikCvHandle* h, const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n,
+int32_t ensure_tables(TrikCvHandle* h, TableSet& t, const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n,
                       hipStream_t s) {
   std::vector<uint32_t> key;
   key.reserve(3 * n + 1);
@@ -277,39 +291,32 @@ int32_t ensure_tables(TrikCvHandle* h, const TRIK_VIDTRANSCODE_CV_InArgsAlg* ran
     const PackedRange p = pack_range(ranges[i]);
     key.push_back(p.from); key.push_back(p.to); key.push_back(p.expect);
   }
-  if (key == h->table_key && h->d_tables) return 0;
+  if (key == t.key && t.d_tables) return 0;
   const int groups = (n + kRangesPerLaunch - 1) / kRangesPerLaunch;
   if (h->tables_busy) HIP_TRY(hipEventSynchronize(h->tables_busy));  // previous users done
-  if (groups > h->table_groups_cap) {
-    (void)hipFree(h->d_tables);
-    (void)hipHostFree(h->h_tables);
-    (void)hipFree(h->d_stripe);
-    (void)hipHostFree(h->h_stripe);
-    h->d_tables = nullptr; h->h_tables = nullptr; h->table_groups_cap = 0;
-    h->d_stripe = nullptr; h->h_stripe = nullptr;
-    HIP_TRY(hipMalloc(&h->d_tables, sizeof(RangeTables) * groups));
-    HIP_TRY(hipHostMalloc(&h->h_tables, sizeof(RangeTables) * groups, hipHostMallocDefault));
-    HIP_TRY(hipMalloc(&h->d_stripe, sizeof(StripeTables) * groups));
-    HIP_TRY(hipHostMalloc(&h->h_stripe, sizeof(StripeTables) * groups, hipHostMallocDefault));
-    h->table_groups_cap = groups;
+  if (groups > t.groups_cap) {
+    t.release();
+    HIP_TRY(hipMalloc(&t.d_tables, sizeof(RangeTables) * groups));
+    HIP_TRY(hipHostMalloc(&t.h_tables, sizeof(RangeTables) * groups, hipHostMallocDefault));
+    HIP_TRY(hipMalloc(&t.d_stripe, sizeof(StripeTables) * groups));
+    HIP_TRY(hipHostMalloc(&t.h_stripe, sizeof(StripeTables) * groups, hipHostMallocDefault));
+    t.groups_cap = groups;
   }
   for (int g = 0; g < groups; ++g) {
     const int cnt = n - g * kRangesPerLaunch < kRangesPerLaunch ? n - g * kRangesPerLaunch : kRangesPerLaunch;
-    compile_tables(ranges + g * kRangesPerLaunch, cnt, &h->h_tables[g]);
-    compile_stripe_tables(h->h_tables[g], cnt, &h->h_stripe[g]);
+    compile_tables(ranges + g * kRangesPerLaunch, cnt, &t.h_tables[g]);
+    compile_stripe_tables(t.h_tables[g], cnt, &t.h_stripe[g]);
   }
-  HIP_TRY(hipMemcpyAsync(h->d_tables, h->h_tables, sizeof(RangeTables) * groups,
-                         hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(h->d_stripe, h->h_stripe, sizeof(StripeTables) * groups,
-                         hipMemcpyHostToDevice, s));
-  h->table_key.swap(key);
+  HIP_TRY(hipMemcpyAsync(t.d_tables, t.h_tables, sizeof(RangeTables) * groups, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(t.d_stripe, t.h_stripe, sizeof(StripeTables) * groups, hipMemcpyHostToDevice, s));
+  t.key.swap(key);
   return 0;
 }
 
 int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
                  const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, TrikHsvTargetSums* sums,
                  uint8_t* masks, hipStream_t s) {
-  int32_t rc = ensure_tables(h, ranges, n, s);
+  int32_t rc = ensure_tables(h, h->sums_tables, ranges, n, s);
   if (rc) return rc;
   if (b->n_frames == 0 || b->width == 0 || b->height == 0) return 0;
   for (int g = 0; g * kRangesPerLaunch < n; ++g) {
@@ -322,8 +329,8 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
     a.n_ranges = n - g * kRangesPerLaunch < kRangesPerLaunch ? n - g * kRangesPerLaunch : kRangesPerLaunch;
     a.range_offset = g * kRangesPerLaunch;
     a.sums_ranges = n;
-    a.tables = h->d_tables + g;
-    a.stripe_tables = h->d_stripe + g;
+    a.tables = h->sums_tables.d_tables + g;
+    a.stripe_tables = h->sums_tables.d_stripe + g;
     a.sums = sums;
     a.masks = masks;
     a.mask_shift = g * kRangesPerLaunch;
@@ -389,18 +396,35 @@ PreviewArgs preview_args(const TrikCvHandle* h, const TrikHsvFrameBatch& b,
   return a;
 }
 
+// The preview's detection range compiled into the single-range tables.
+int32_t preview_tables(TrikCvHandle* h, PreviewArgs& pa, const TRIK_VIDTRANSCODE_CV_InArgsAlg& range,
+                       hipStream_t s) {
+  int32_t rc = ensure_tables(h, h->single_tables, &range, 1, s);
+  if (rc) return rc;
+  pa.range = pack_range(range);
+  pa.tables = h->single_tables.d_stripe;
+  return 0;
+}
+
+// The line sensor's range in the object sensor's terms: hue 0..359 and
+// saturation 0..100 scale to the full 0..255 bytes LSEQ:391-396 fixes.
+TRIK_VIDTRANSCODE_CV_InArgsAlg line_alg(int val_from, int val_to) {
+  TRIK_VIDTRANSCODE_CV_InArgsAlg r;
+  memset(&r, 0, sizeof r);
+  r.detectHueFrom = 0;
+  r.detectHueTo = 359;
+  r.detectSatFrom = 0;
+  r.detectSatTo = 100;
+  r.detectValFrom = (uint8_t)val_from;
+  r.detectValTo = (uint8_t)val_to;
+  return r;
+}
+
 // LSEQ:391-414: hue and saturation bounds fixed at 0..255 (unscaled), value
 // scaled as the object sensor's.
 uint32_t scale_val(int v) {
   const int s = (v * 255) / 100;
   return (uint32_t)(s < 0 ? 0 : (s > 255 ? 255 : s));
-}
-PackedRange line_range(int val_from, int val_to) {
-  PackedRange r;
-  r.from = scale_val(val_from) << 16;
-  r.to = (scale_val(val_to) << 16) | 0xFFFFu;
-  r.expect = 0;
-  return r;
 }
 LineArgs line_args(const TrikHsvFrameBatch& b, int val_from, int val_to, int band_start, int band_stop,
                    TrikHsvTargetSums* sums, TrikHsvTarget* targets) {
@@ -470,14 +494,14 @@ int32_t ensure_blob_scratch(TrikCvHandle* h, int n, int w, int hgt) {
 int32_t blob_args(TrikCvHandle* h, const TrikHsvFrameBatch& b, const TRIK_VIDTRANSCODE_CV_InArgsAlg& range,
                   TrikHsvTarget* targets, int32_t* top, uint8_t* meta, uint16_t* labels, int32_t* n_labels,
                   hipStream_t s, BlobArgs& a) {
-  int32_t rc = ensure_tables(h, &range, 1, s);
+  int32_t rc = ensure_tables(h, h->single_tables, &range, 1, s);
   if (rc) return rc;
   a.frames = static_cast<const uint8_t*>(b.frames);
   a.frame_stride = b.frame_stride;
   a.n_frames = b.n_frames;
   a.width = b.width; a.height = b.height; a.line_length = b.line_length;
   a.range = pack_range(range);
-  a.tables = h->d_stripe;
+  a.tables = h->single_tables.d_stripe;
   a.aligned4 = (reinterpret_cast<uintptr_t>(b.frames) & 3) == 0 && (b.n_frames <= 1 || (b.frame_stride & 3) == 0) &&
                (b.line_length & 3) == 0;
   a.meta = meta ? meta : h->d_meta;
@@ -732,7 +756,8 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
             int32_t r = ensure_maps(h, h->in_w, h->in_h, h->out_w, h->out_h, h->stream, 5, h->in_w - 5);
             if (r) return r;
             PreviewArgs pa = preview_args(h, b, ia, h->out_w, h->out_h, h->out_ll, h->d_preview, (int64_t)pb);
-            pa.range = line_range(ia.detectValFrom, ia.detectValTo);
+            r = preview_tables(h, pa, line_alg(ia.detectValFrom, ia.detectValTo), h->stream);
+            if (r) return r;
             HIP_TRY(launch_preview_body(pa, h->stream));
             HIP_TRY(launch_line_overlay(pa, h->d_sums, h->stream));
             HIP_TRY(hipMemcpyAsync(out_ptr, h->d_preview, pb, hipMemcpyDeviceToHost, h->stream));
@@ -768,8 +793,10 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
           }
           r = ensure_maps(h, h->in_w, h->in_h, h->out_w, h->out_h, h->stream);
           if (r) return r;
-          const PreviewArgs pa = preview_args(h, b, in_args->alg, h->out_w, h->out_h, h->out_ll,
-                                              h->d_preview, (int64_t)pb);
+          PreviewArgs pa = preview_args(h, b, in_args->alg, h->out_w, h->out_h, h->out_ll, h->d_preview,
+                                        (int64_t)pb);
+          r = preview_tables(h, pa, in_args->alg, h->stream);
+          if (r) return r;
           HIP_TRY(launch_preview(pa, h->d_sums, 1, h->stream));
           HIP_TRY(hipMemcpyAsync(out_ptr, h->d_preview, pb, hipMemcpyDeviceToHost, h->stream));
         }
@@ -895,8 +922,10 @@ extern "C" int32_t trik_hsv_batch_preview(TRIK_VIDTRANSCODE_CV_Handle h, const T
   // the preview kernel writes every byte of each preview, zeros included (WFXNS:234)
   rc = ensure_maps(h, b->width, b->height, out_width, out_height, s);
   if (rc) return rc;
-  HIP_TRY(launch_preview(preview_args(h, *b, *range, out_width, out_height, out_line_length, previews,
-                                      preview_stride), sums, sums_pitch, s));
+  PreviewArgs pa = preview_args(h, *b, *range, out_width, out_height, out_line_length, previews, preview_stride);
+  rc = preview_tables(h, pa, *range, s);
+  if (rc) return rc;
+  HIP_TRY(launch_preview(pa, sums, sums_pitch, s));
   if (!h->tables_busy) HIP_TRY(hipEventCreateWithFlags(&h->tables_busy, hipEventDisableTiming));
   HIP_TRY(hipEventRecord(h->tables_busy, s));
   return 0;
@@ -952,7 +981,8 @@ extern "C" int32_t trik_hsv_line_preview(TRIK_VIDTRANSCODE_CV_Handle h, const Tr
   TRIK_VIDTRANSCODE_CV_InArgsAlg ia;
   memset(&ia, 0, sizeof ia);
   PreviewArgs pa = preview_args(h, *b, ia, out_width, out_height, out_line_length, previews, preview_stride);
-  pa.range = line_range(val_from, val_to);
+  rc = preview_tables(h, pa, line_alg(val_from, val_to), s);
+  if (rc) return rc;
   HIP_TRY(launch_preview_body(pa, s));
   HIP_TRY(launch_line_overlay(pa, sums, s));
   if (!h->tables_busy) HIP_TRY(hipEventCreateWithFlags(&h->tables_busy, hipEventDisableTiming));

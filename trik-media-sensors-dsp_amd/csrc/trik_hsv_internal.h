@@ -80,6 +80,7 @@ struct PreviewArgs {
   int64_t frame_stride;
   int32_t n_frames, width, height, line_length, layout;
   PackedRange range;          // the preview's range (WSEQ:425-445)
+  const StripeTables* tables = nullptr;  // that range compiled as range 0 (device)
   int32_t aligned4;           // frames, strides, line lengths and previews 4-byte aligned
   int32_t out_w, out_h, out_ll;
   uint8_t* previews;

@@ -2,7 +2,7 @@
 // (SURVEY 8(f) rows 1 and 2), paths relative to the reference checkout, WSEQ
 // as in include/trik_hsv.h:
 //
-//  preview_kernel     the RGB565X preview stream written by proceedImageHsv
+//  preview_gather_kernel  the RGB565X preview stream written by proceedImageHsv
 //                     (WSEQ:316-354): every source pixel is written through the
 //                     truncated scale maps (WSEQ:371-387), last writer wins, a
 //                     detected pixel as 0x00ffff.  Computed as a gather: output
@@ -25,6 +25,7 @@
 
 #include "trik_hsv_internal.h"
 #include "trik_hsv_pixel.h"
+#include "trik_hsv_stripe_px.h"
 
 namespace trik_hsv {
 
@@ -44,68 +45,73 @@ constexpr Luts make_luts() {  // WSEQ:400-406
 __constant__ Luts c_luts = make_luts();
 
 
-// One pixel of the preview: RGB565X of (det ? 0x00ffff : rgb888), WSEQ:347;
-// det from the range, or from the metapixel flag when meta_det >= 0 (OSEQ:411-413).
-__device__ __forceinline__ uint32_t preview_px(int Y, int U, int V, const PackedRange& range, int meta_det) {
-  const PixelRgb p = pixel_rgb(Y, U, V);
-  if (meta_det >= 0) {
-    const uint32_t rgb = meta_det ? 0x00ffffu : p.rgb888();
-    return ((rgb >> 19) & 0x001fu) | ((rgb >> 5) & 0x07e0u) | ((rgb << 8) & 0xf800u);
+// The preview as a grid-stride gather over 4-byte output groups (two output
+// pixels each) of the whole batch: 1024-lane workgroups, two per CU, the
+// single range's StripeTables image at LDS address 0 and the hot kernel's
+// per-pixel arithmetic (phase1 also yields the clamped colour); with
+// a.meta set (the multi-blob preview) detection is the metapixel flag and no
+// tables are staged.  Every byte of the out_h x out_ll preview is written.
+struct PreviewGeom {
+  FastDiv per_frame;  // out_h * quads per row
+  FastDiv per_row;    // quads per row
+  uint32_t total;
+};
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8)))
+void preview_gather_kernel(PreviewArgs a, PreviewGeom g) {
+  using namespace stripe_px;
+  if (!a.meta) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4* src = reinterpret_cast<const u32x4*>(a.tables);
+    typedef __attribute__((address_space(3))) u32x4* lds_u128_wptr;
+    lds_u128_wptr dst = (lds_u128_wptr)(uintptr_t)0;
+    for (int i = threadIdx.x; i < (int)(sizeof(StripeTables) / 16); i += blockDim.x) dst[i] = src[i];
   }
-  const int mx = max(p.r, max(p.g, p.b)), mn = min(p.r, min(p.g, p.b));
-  const int m = c_luts.l43[mx - mn];
-  int h;
-  if (mx == p.g) h = 21845 + m * (p.b - p.r);
-  else if (mx == p.b) h = 43690 + m * (p.r - p.g);
-  else h = m * (p.g - p.b);
-  const uint32_t H = ((uint32_t)h >> 8) & 0xFFu;
-  const uint32_t S = ((uint32_t)c_luts.l255[mx] * (uint32_t)(mx - mn)) >> 8;
-  const uint32_t rgb = detect_packed(H, S, (uint32_t)mx, range) ? 0x00ffffu : p.rgb888();
-  return ((rgb >> 19) & 0x001fu) | ((rgb >> 5) & 0x07e0u) | ((rgb << 8) & 0xf800u);
-}
-
-// A wave per output row (4 rows per workgroup, frame and row from the block
-// index), a lane per 4 output bytes (two pixels).  Every byte of the out_h x
-// out_ll preview is written -- pixels no source pixel maps to and the line
-// padding as zero -- so the zero fill of WFXNS:234 needs no memset.
-constexpr int kPreviewRows = 4;
-__global__ __launch_bounds__(64 * kPreviewRows) void preview_kernel(PreviewArgs a) {
-  const int groups = (a.out_h + kPreviewRows - 1) / kPreviewRows;
-  const int f = blockIdx.x / groups;
-  const int r = (blockIdx.x - f * groups) * kPreviewRows + threadIdx.y;
-  if (r >= a.out_h) return;
-  const int quads = (a.out_ll + 3) >> 2;  // 4-byte groups per output row
-  uint8_t* row = a.previews + (int64_t)f * a.preview_stride + (int64_t)r * a.out_ll;
-  const uint8_t* fr = a.frames + (int64_t)f * a.frame_stride;
-  const int sr = a.last_row[r];
-  for (int q = threadIdx.x; q < quads; q += 64) {
-  uint32_t v[2] = {0u, 0u};
+  __syncthreads();
+  const int t = threadIdx.x;
+  const uint32_t hue_lane = (uint32_t)offsetof(StripeTables, hue) + ((t % kHueCopies) << 2);
+  const uint32_t m43_lane = (uint32_t)offsetof(StripeTables, m43) + ((t % kM43Copies) << 2);
+  const uint32_t qpr = g.per_row.d;
+  const int64_t ll = a.line_length;
+  for (uint32_t i = blockIdx.x * blockDim.x + t; i < g.total; i += gridDim.x * blockDim.x) {
+    const uint32_t f = fdiv(i, g.per_frame), rem = i - f * g.per_frame.d;
+    const uint32_t r = fdiv(rem, g.per_row), q = rem - r * qpr;
+    const uint8_t* fr = a.frames + (int64_t)f * a.frame_stride;
+    const int sr = a.last_row[r];
+    uint32_t v[2] = {0u, 0u};
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int c = 2 * q + k;
-    if (c >= a.out_w || sr < 0) continue;
-    const int sc = a.last_col[c];
-    if (sc < 0) continue;
-    int Y, U, V;
-    if (a.layout == TRIK_HSV_LAYOUT_YUYV && a.aligned4) {
-      const uint32_t w = *reinterpret_cast<const uint32_t*>(fr + (int64_t)sr * a.line_length + 4 * (sc >> 1));
-      Y = (w >> (16 * (sc & 1))) & 0xFF;
-      U = (w >> 8) & 0xFF;
-      V = w >> 24;
-    } else {
-      fetch_yuv(fr, a.height, a.line_length, a.layout, sr, sc, Y, U, V);
+    for (int k = 0; k < 2; ++k) {
+      const int c = 2 * (int)q + k;
+      if (c >= a.out_w || sr < 0) continue;
+      const int sc = a.last_col[c];
+      if (sc < 0) continue;
+      uint32_t w;  // the pixel as a YUYV word with its Y in byte 0
+      if (a.layout == TRIK_HSV_LAYOUT_YUYV && a.aligned4) {
+        w = *reinterpret_cast<const uint32_t*>(fr + (int64_t)sr * ll + 4 * (sc >> 1));
+        if (sc & 1) w = __builtin_amdgcn_perm(w, w, 0x03020102u);
+      } else {
+        int Y, U, V;
+        fetch_yuv(fr, a.height, a.line_length, a.layout, sr, sc, Y, U, V);
+        w = (uint32_t)Y | ((uint32_t)U << 8) | ((uint32_t)V << 24);
+      }
+      const Phase1 p = phase1<0>(w, w ^ 0xFF00FF00u, m43_lane);
+      uint32_t det;
+      if (a.meta) {
+        det = a.meta[((int64_t)f * (a.height >> 2) + (sr >> 2)) * (a.width >> 2) + (sc >> 2)];
+      } else {
+        const uint32_t m = lds_u32(p.m43_addr), sv = lds_u8(p.sv_addr);
+        det = combine(lds_u32(phase2_addr(m, p, hue_lane)), sv) & 1u;
+      }
+      const uint32_t rgb = det ? 0x00ffffu : p.rgb888;
+      v[k] = ((rgb >> 19) & 0x001fu) | ((rgb >> 5) & 0x07e0u) | ((rgb << 8) & 0xf800u);
     }
-    const int meta_det =
-        a.meta ? (int)a.meta[((int64_t)f * (a.height >> 2) + (sr >> 2)) * (a.width >> 2) + (sc >> 2)] : -1;
-    v[k] = preview_px(Y, U, V, a.range, meta_det);
-  }
-  const int b0 = 4 * q;
-  if (a.aligned4 && b0 + 4 <= a.out_ll) {
-    *reinterpret_cast<uint32_t*>(row + b0) = v[0] | (v[1] << 16);
-  } else {
-    const uint8_t bytes[4] = {(uint8_t)v[0], (uint8_t)(v[0] >> 8), (uint8_t)v[1], (uint8_t)(v[1] >> 8)};
-    for (int k = 0; k < 4 && b0 + k < a.out_ll; ++k) row[b0 + k] = bytes[k];
-  }
+    uint8_t* row = a.previews + (int64_t)f * a.preview_stride + (int64_t)r * a.out_ll;
+    const int b0 = 4 * (int)q;
+    if (a.aligned4 && b0 + 4 <= a.out_ll) {
+      *reinterpret_cast<uint32_t*>(row + b0) = v[0] | (v[1] << 16);
+    } else {
+      const uint8_t bytes[4] = {(uint8_t)v[0], (uint8_t)(v[0] >> 8), (uint8_t)v[1], (uint8_t)(v[1] >> 8)};
+      for (int k = 0; k < 4 && b0 + k < a.out_ll; ++k) row[b0 + k] = bytes[k];
+    }
   }
 }
 
@@ -230,20 +236,42 @@ __global__ __launch_bounds__(kRangeBlock) void auto_range_kernel(AutoRangeArgs a
 
 }  // namespace
 
+static int launch_gather(const PreviewArgs& a, hipStream_t s) {
+  const int64_t qpr = (a.out_ll + 3) / 4, total = (int64_t)a.n_frames * a.out_h * qpr;
+  if (total >= (1ll << 31) || (!a.meta && !a.tables)) return hipErrorInvalidValue;
+  if (total == 0) return hipSuccess;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(preview_gather_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(StripeTables));
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  PreviewGeom g;
+  g.per_frame = make_div((uint32_t)(a.out_h * qpr));
+  g.per_row = make_div((uint32_t)qpr);
+  g.total = (uint32_t)total;
+  const int64_t blocks = (total + 1023) / 1024, slots = 2LL * cus;
+  hipLaunchKernelGGL(preview_gather_kernel, dim3((unsigned)(blocks < slots ? blocks : slots)), dim3(1024),
+                     a.meta ? 0 : sizeof(StripeTables), s, a, g);
+  return hipGetLastError();
+}
+
 int launch_preview_body(const PreviewArgs& a, hipStream_t s) {
   if (a.n_frames <= 0 || a.out_w <= 0 || a.out_h <= 0) return hipSuccess;
-  const int64_t blocks = (int64_t)a.n_frames * ((a.out_h + kPreviewRows - 1) / kPreviewRows);
-  if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(preview_kernel, dim3((unsigned)blocks), dim3(64, kPreviewRows), 0, s, a);
-  return hipGetLastError();
+  return launch_gather(a, s);
 }
 
 int launch_preview(const PreviewArgs& a, const TrikHsvTargetSums* sums, int sums_pitch, hipStream_t s) {
   if (a.n_frames <= 0 || a.out_w <= 0 || a.out_h <= 0) return hipSuccess;
-  const int64_t blocks = (int64_t)a.n_frames * ((a.out_h + kPreviewRows - 1) / kPreviewRows);
-  if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(preview_kernel, dim3((unsigned)blocks), dim3(64, kPreviewRows), 0, s, a);
-  hipError_t e = hipGetLastError();
+  hipError_t e = (hipError_t)launch_gather(a, s);
   if (e != hipSuccess || a.width <= 0 || a.height <= 0) return e;
   hipLaunchKernelGGL(overlay_kernel, dim3((unsigned)a.n_frames), dim3(64), 0, s, a, sums, sums_pitch);
   return hipGetLastError();

@@ -125,6 +125,21 @@ __device__ __forceinline__ void draw_guides(const Canvas& cv, int lane, int nlan
   }
 }
 
+// x / d for 32-bit x via a host-computed multiplier (round-up method):
+// q = (umulhi(x, magic) + x) >> shift, exact for every 32-bit x.
+struct FastDiv {
+  uint32_t magic, shift, d;
+};
+inline FastDiv make_div(uint32_t d) {
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  const uint64_t m = ((1ull << 32) * ((1ull << s) - d)) / d + 1;
+  return FastDiv{(uint32_t)m, s, d};
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
+  return (uint32_t)(((uint64_t)__umulhi(x, f.magic) + x) >> f.shift);
+}
+
 // (Y, U, V) of pixel `col` of row `row`: packed YUYV (WSEQ:262-270) or the
 // ov7670 planes (OSEQ:360-373: U = odd chroma byte, V = even chroma byte).
 __device__ __forceinline__ void fetch_yuv(const uint8_t* frame, int height, int line_length, int layout,
