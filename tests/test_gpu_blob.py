@@ -167,3 +167,29 @@ def test_blob_rejects(hsv):
         assert empty["targets"].shape == (0, 8, 4)
     finally:
         det.close()
+
+
+def test_blob_sensor_empty_frame(hsv):
+    """0 x 0 input: no bitmap, no clusters; target[] zeroed (OSEQ:563)."""
+    s = hsv.BlobSensor(hsv._default_params(1, hsv.FORMAT_YUV422P))
+    try:
+        assert s.set_params(0, 0, 0, out_width=0, out_height=0, out_line_length=0) == 0
+        out = np.full(16, 0xCD, np.uint8)
+        rc, oa = s.process(np.zeros(16, np.uint8), RED, out_buffer=out)
+        assert rc == 0
+        assert all((oa.alg.target[i].x, oa.alg.target[i].y, oa.alg.target[i].size) == (0, 0, 0) for i in range(8))
+        assert not out.any()
+    finally:
+        s.close()
+
+
+def test_blob_batch_zero_size_frames(hsv):
+    import torch
+
+    det = hsv.Detector()
+    try:
+        dev = torch.zeros(64, dtype=torch.uint8, device="cuda")
+        res = det.blob_batch(dev, 0, 0, 0, RED, n_frames=3, frame_stride=0)
+        assert not res["targets"].any() and not res["top"].any() and not res["n_labels"].any()
+    finally:
+        det.close()

@@ -210,3 +210,16 @@ def test_line_rejects(hsv, oracle_mod):
         assert sums.shape == (0, 3) and targets.shape == (0, 4)
     finally:
         s.close()
+
+
+def test_line_sensor_empty_frame(hsv):
+    """0 x 0 input: run() skips the image (LSEQ:420); targets 0, preview untouched zeros."""
+    s = hsv.LineSensor(hsv._default_params(1, hsv.FORMAT_YUV422P))
+    try:
+        assert s.set_params(0, 0, 0, out_width=0, out_height=0, out_line_length=0) == 0
+        out = np.full(16, 0xCD, np.uint8)
+        rc, oa = s.process(np.zeros(16, np.uint8), (0, 359, 0, 100, 0, 30), out_buffer=out)
+        assert rc == 0 and (oa.alg.targetX, oa.alg.targetY, oa.alg.targetSize) == (0, 0, 0)
+        assert not out.any()
+    finally:
+        s.close()
