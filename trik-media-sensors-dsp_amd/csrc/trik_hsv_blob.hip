@@ -109,6 +109,40 @@ void blob_meta_kernel(BlobArgs a, MetaGeom g) {
 
 constexpr uint32_t kInf = 0xFFFFu;
 
+// Inclusive wave scans with DPP (row_shr 1/2/4/8 inside 16-lane rows, then
+// row_bcast 15/31 across rows): VALU-latency steps instead of LDS permutes.
+// A lane whose source is outside its row (or whose row is masked) reads the
+// operator's identity.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_from(uint32_t identity, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)identity, (int)v, CTRL, ROWS, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+  v += dpp_from<0x111, 0xF>(0u, v);
+  v += dpp_from<0x112, 0xF>(0u, v);
+  v += dpp_from<0x114, 0xF>(0u, v);
+  v += dpp_from<0x118, 0xF>(0u, v);
+  v += dpp_from<0x142, 0xA>(0u, v);
+  v += dpp_from<0x143, 0xC>(0u, v);
+  return v;
+}
+// segmented minimum over (break, min) pairs: (b1, m1) then (b2, m2) combine to
+// (b1 | b2, b2 ? m2 : min(m1, m2))
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void seg_step(uint32_t& b, uint32_t& m) {
+  const uint32_t tb = dpp_from<CTRL, ROWS>(0u, b), tm = dpp_from<CTRL, ROWS>(kInf, m);
+  m = b ? m : min(tm, m);
+  b |= tb;
+}
+__device__ __forceinline__ void wave_incl_segmin(uint32_t& b, uint32_t& m) {
+  seg_step<0x111, 0xF>(b, m);
+  seg_step<0x112, 0xF>(b, m);
+  seg_step<0x114, 0xF>(b, m);
+  seg_step<0x118, 0xF>(b, m);
+  seg_step<0x142, 0xA>(b, m);
+  seg_step<0x143, 0xC>(b, m);
+}
+
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -131,23 +165,25 @@ __device__ __forceinline__ bool blob_target(int32_t size, int32_t sx, int32_t sy
   return true;
 }
 
+// Register form: lane l owns columns c0 = l*K .. c0+K-1 (K <= KMAX) and keeps
+// their set flags, up-row minima and the labels of rows r-1 / r in registers
+// (fully unrolled loops over KMAX with a j < K guard); the boundary values of
+// the neighbouring lanes come by one-lane shuffles.  LDS holds eq (and the
+// staged bitmap).
+template <int KMAX>
 __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
   extern __shared__ uint16_t smem[];
   const int f = blockIdx.x, lane = threadIdx.x;
   const int bw = a.width >> 2, bh = a.height >> 2;
   const int ml = a.max_labels;
-  uint16_t* eq = smem;                          // [ml]
-  uint16_t* prev = eq + ((ml + 1) & ~1);        // [bw] labels of row r-1
-  uint16_t* cur = prev + bw;                    // [bw] labels of row r
-  uint16_t* up = cur + bw;                      // [bw] up-row minimum, kInf if none
-  uint8_t* dset = reinterpret_cast<uint8_t*>(up + bw);  // [bw] set flags of row r
+  uint16_t* eq = smem;  // [ml]
   // the frame's bitmap: staged in LDS when it fits (bw*bh is a multiple of 8)
   const uint8_t* meta = a.meta + (int64_t)f * bw * bh;
   if (a.meta_lds) {
-    uint32_t* dst = reinterpret_cast<uint32_t*>(dset + bw);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(eq + ((ml + 1) & ~1));
     const uint32_t* src = reinterpret_cast<const uint32_t*>(meta);
     for (int i = lane; i < bw * bh / 4; i += 64) dst[i] = src[i];
-    meta = dset + bw;
+    meta = reinterpret_cast<const uint8_t*>(dst);
     __syncthreads();
   }
   // own[3k + {0,1,2}] = x, y, size (zeroed by the launcher); fin: folded
@@ -155,96 +191,110 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
   int32_t* fin = a.stats + ((int64_t)a.n_frames + f) * 3 * ml;
   uint16_t* labels = a.labels ? a.labels + (int64_t)f * bw * bh : nullptr;
 
-  const int K = (bw + 63) / 64;  // columns per lane, contiguous
-  const int c0 = lane * K, c1 = min(c0 + K, bw);
-  for (int c = lane; c < bw; c += 64) prev[c] = 0;
+  const int K = (bw + 63) / 64;
+  const int c0 = lane * K;
+  uint32_t prv[KMAX], cur[KMAX], dd[KMAX], up[KMAX];
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j) prv[j] = 0;
   if (lane == 0) eq[0] = 0;
   int next = 1;  // next new label (wave-uniform)
   for (int r = 0; r < bh; ++r) {
-    // phase 1: set flags and up-row minima (CLU:70-84)
-    for (int c = lane; c < bw; c += 64) {
-      const uint8_t d = meta[(int64_t)r * bw + c];
-      dset[c] = d;
-      uint32_t u = kInf;
-      if (d && r > 0) {
-        const uint32_t p0 = c > 0 ? prev[c - 1] : 0u, p1 = prev[c], p2 = c < bw - 1 ? prev[c + 1] : 0u;
-        if (p0) u = p0;
-        if (p1 && p1 < u) u = p1;
-        if (p2 && p2 < u) u = p2;
-      }
-      up[c] = (uint16_t)u;
-    }
-    __syncthreads();
-    // phase 2: opening metapixels (set, no set causal neighbour) get new labels
-    // numbered in raster order: an exclusive prefix sum of the lanes' counts
-    uint32_t nseed = 0;
-    for (int c = c0; c < c1; ++c)
-      if (dset[c] && !(c > 0 && dset[c - 1]) && up[c] == kInf) ++nseed;
-    uint32_t incl = nseed;
+    const uint8_t* mrow = meta + (int64_t)r * bw;
+    uint32_t prev_last = 0, d_last = 0;
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t o = __shfl_up(incl, off, 64);
-      if (lane >= off) incl += o;
+    for (int j = 0; j < KMAX; ++j) {
+      const int c = c0 + j;
+      dd[j] = (j < K && c < bw) ? (uint32_t)mrow[c] : 0u;
+      if (j == K - 1) {
+        prev_last = prv[j];
+        d_last = dd[j];
+      }
     }
-    const uint32_t total = __shfl(incl, 63, 64);
+    // the neighbours' boundary columns (CLU:70-84 reads c-1 and c+1)
+    uint32_t l_prev = __shfl_up(prev_last, 1, 64), l_d = __shfl_up(d_last, 1, 64);
+    uint32_t r_prev = __shfl_down(prv[0], 1, 64);
+    if (lane == 0) l_prev = l_d = 0;
+    if (lane == 63) r_prev = 0;
+    // up-row minima of the set metapixels; opening ones (no set causal neighbour)
+    uint32_t nseed = 0;
+    {
+      uint32_t left = l_d;
+#pragma unroll
+      for (int j = 0; j < KMAX; ++j) {
+        const uint32_t pl = j == 0 ? l_prev : prv[j > 0 ? j - 1 : 0];
+        const uint32_t pr = j + 1 < K ? prv[j + 1 < KMAX ? j + 1 : j] : r_prev;
+        uint32_t u = kInf;
+        if (dd[j] && r > 0) {
+          if (pl) u = pl;
+          if (prv[j] && prv[j] < u) u = prv[j];
+          if (pr && pr < u) u = pr;
+        }
+        up[j] = u;
+        if (j < K && dd[j] && !left && u == kInf) ++nseed;
+        left = dd[j];
+      }
+    }
+    // new labels in raster order: exclusive prefix sum of the lanes' counts
+    const uint32_t incl = wave_incl_sum(nseed);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     const uint32_t label_next = (uint32_t)next + incl - nseed;
     // segmented min-scan over runs of set metapixels: this lane's summary is
     // (the chunk holds an unset one, the minimum after the last unset one)
     uint32_t cb = 0, cm = kInf;
     {
-      uint32_t lbl = label_next;
-      for (int c = c0; c < c1; ++c) {
-        if (!dset[c]) {
-          cb = 1;
-          cm = kInf;
-        } else {
-          const bool open = !(c > 0 && dset[c - 1]) && up[c] == kInf;
-          cm = min(cm, open ? lbl++ : (uint32_t)up[c]);
-        }
-      }
-    }
+      uint32_t lbl = label_next, left = l_d;
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {  // inclusive scan of (break, min) pairs
-      const uint32_t ob = __shfl_up(cb, off, 64), om = __shfl_up(cm, off, 64);
-      if (lane >= off) {
-        cm = cb ? cm : min(om, cm);
-        cb = cb | ob;
+      for (int j = 0; j < KMAX; ++j) {
+        if (j < K) {
+          if (!dd[j]) {
+            cb = 1;
+            cm = kInf;
+          } else {
+            const bool open = !left && up[j] == kInf;
+            cm = min(cm, open ? lbl++ : up[j]);
+          }
+        }
+        left = dd[j];
       }
     }
+    wave_incl_segmin(cb, cm);
     uint32_t carry = __shfl_up(cm, 1, 64);  // exclusive: lanes before this one
     if (lane == 0) carry = kInf;
-    // phase 3: labels; open the new labels (eq[L] = L, zero sums)
+    // labels; open the new labels (eq[L] = L)
+    uint32_t seeds = 0, cur_last = 0;
     {
-      uint32_t lbl = label_next, run = carry;
-      for (int c = c0; c < c1; ++c) {
-        const bool d = dset[c] != 0;
-        const bool left = c > 0 && dset[c - 1] != 0;
-        if (!d) {
+      uint32_t lbl = label_next, run = carry, left = l_d;
+#pragma unroll
+      for (int j = 0; j < KMAX; ++j) {
+        if (!dd[j]) {
           run = kInf;
-          cur[c] = 0;
-          continue;
-        }
-        if (!left && up[c] == kInf) {  // CLU:98-112
+          cur[j] = 0;
+        } else if (!left && up[j] == kInf) {  // CLU:98-112
           eq[lbl] = (uint16_t)lbl;
+          seeds |= 1u << j;
           run = lbl++;
+          cur[j] = run;
         } else {
-          run = min(run, (uint32_t)up[c]);
+          run = min(run, up[j]);
+          cur[j] = run;
         }
-        cur[c] = (uint16_t)run;
+        left = dd[j];
+        if (j == K - 1) cur_last = cur[j];
       }
     }
     next += (int)total;
-    __syncthreads();
-    // phase 4: statistics of the non-opening metapixels, one atomic per run of
-    // equal labels; equivalence events flagged
+    uint32_t l_cur = __shfl_up(cur_last, 1, 64);
+    if (lane == 0) l_cur = 0;
+    // statistics of the non-opening metapixels, one atomic per run of equal
+    // labels; equivalence events flagged
     uint32_t events = 0;  // bit j: column c0 + j has a neighbour label != L
     {
       uint32_t acc_l = 0;
       int32_t ax = 0, ay = 0, an = 0;
-      for (int c = c0; c < c1; ++c) {
-        const uint32_t L = cur[c];
-        const bool seed = L != 0 && !(c > 0 && dset[c - 1]) && up[c] == kInf;
-        if (L && !seed) {
+#pragma unroll
+      for (int j = 0; j < KMAX; ++j) {
+        const uint32_t L = cur[j];
+        if (L && !((seeds >> j) & 1u)) {
           if (L != acc_l) {
             if (an) {
               atomicAdd(&own[3 * acc_l], ax);
@@ -254,17 +304,16 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
             acc_l = L;
             ax = ay = an = 0;
           }
-          ax += c;
+          ax += c0 + j;
           ay += r;
           ++an;
-          const uint32_t n0 = c > 0 ? cur[c - 1] : 0u;
-          const uint32_t n1 = (r > 0 && c > 0) ? prev[c - 1] : 0u;
-          const uint32_t n2 = r > 0 ? prev[c] : 0u;
-          const uint32_t n3 = (r > 0 && c < bw - 1) ? prev[c + 1] : 0u;
-          if ((n0 && n0 != L) || (n1 && n1 != L) || (n2 && n2 != L) || (n3 && n3 != L))
-            events |= 1u << (c - c0);
+          const uint32_t n0 = j == 0 ? l_cur : cur[j > 0 ? j - 1 : 0];
+          const uint32_t n1 = j == 0 ? l_prev : prv[j > 0 ? j - 1 : 0];
+          const uint32_t n2 = prv[j];
+          const uint32_t n3 = j + 1 < K ? prv[j + 1 < KMAX ? j + 1 : j] : r_prev;
+          if ((n0 && n0 != L) || (n1 && n1 != L) || (n2 && n2 != L) || (n3 && n3 != L)) events |= 1u << j;
         }
-        if (labels) labels[(int64_t)r * bw + c] = (uint16_t)L;
+        if (labels && j < K && c0 + j < bw) labels[(int64_t)r * bw + c0 + j] = (uint16_t)L;
       }
       if (an) {
         atomicAdd(&own[3 * acc_l], ax);
@@ -272,29 +321,29 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
         atomicAdd(&own[3 * acc_l + 2], an);
       }
     }
-    // equivalence events in raster order: lane by lane, each lane in column order
+    // equivalence events in raster order: lane by lane, each lane in column
+    // order (CLU:92-96 as eq[a] = eq[L] for every non-zero neighbour a)
     uint64_t pending = __ballot(events != 0);
     while (pending) {
       const int l = __ffsll((unsigned long long)pending) - 1;
       pending &= pending - 1;
       if (lane == l) {
-        for (uint32_t ev = events; ev; ev &= ev - 1) {
-          const int c = c0 + __ffs(ev) - 1;
-          const uint32_t L = cur[c];
-          const uint16_t e = eq[L];
-          const uint32_t nb[4] = {c > 0 ? cur[c - 1] : 0u, (r > 0 && c > 0) ? prev[c - 1] : 0u,
-                                  r > 0 ? prev[c] : 0u, (r > 0 && c < bw - 1) ? prev[c + 1] : 0u};
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+          if (!((events >> j) & 1u)) continue;
+          const uint16_t e = eq[cur[j]];
+          const uint32_t nb[4] = {j == 0 ? l_cur : cur[j > 0 ? j - 1 : 0],
+                                  j == 0 ? l_prev : prv[j > 0 ? j - 1 : 0], prv[j],
+                                  j + 1 < K ? prv[j + 1 < KMAX ? j + 1 : j] : r_prev};
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            if (nb[i]) eq[nb[i]] = e;  // CLU:92-96
+            if (nb[i]) eq[nb[i]] = e;
         }
       }
       __builtin_amdgcn_wave_barrier();
     }
-    __syncthreads();
-    uint16_t* t = prev;
-    prev = cur;
-    cur = t;
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) prv[j] = cur[j];
   }
   __threadfence();
   __syncthreads();
@@ -412,12 +461,15 @@ int launch_blob(const BlobArgs& a, hipStream_t s) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  size_t lds = sizeof(uint16_t) * ((size_t)((a.max_labels + 1) & ~1) + 3 * (size_t)bw) + (size_t)bw;
+  size_t lds = sizeof(uint16_t) * (size_t)((a.max_labels + 1) & ~1);
   if (lds > 64 * 1024) return hipErrorInvalidValue;
   BlobArgs b = a;
   b.meta_lds = lds + (size_t)bw * bh <= 40 * 1024 ? 1 : 0;  // keep ~4 frames per CU resident
   if (b.meta_lds) lds += (size_t)bw * bh;
-  hipLaunchKernelGGL(blob_ccl_kernel, dim3((unsigned)a.n_frames), dim3(64), lds, s, b);
+  const int K = (bw + 63) / 64;
+  auto kern = K <= 1 ? blob_ccl_kernel<1> : K <= 2 ? blob_ccl_kernel<2> : K <= 4 ? blob_ccl_kernel<4>
+            : K <= 8 ? blob_ccl_kernel<8> : K <= 16 ? blob_ccl_kernel<16> : blob_ccl_kernel<32>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)a.n_frames), dim3(64), lds, s, b);
   return hipGetLastError();
 }
 
