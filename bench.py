@@ -115,10 +115,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (not used by the driver): several ranks on one GPU over gloo
+    local = int(os.environ.get("TRIK_BENCH_DEVICE", local))
+    backend = os.environ.get("TRIK_BENCH_BACKEND", "nccl")  # nccl = RCCL over xGMI
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     W, H, F, T = args.width, args.height, args.frames, args.targets
     ll = 2 * W
@@ -177,7 +183,8 @@ def main():
         "data": "synthetic: device SplitMix64 uniform bytes, seed 0x7A1C" if args.kind == 0
                 else "synthetic: device scene generator (gradients + 6 discs), seed 0x7A1C",
         "config": {"workload": f"C3: batch {F} x {W}x{H} YUYV per GPU, {T} HSV targets"
-                               + (f" (C5 at N=8: {F * world} frames)" if world > 1 else ""),
+                               + (f"; {F * world} frames over {world} GPUs" + (" (C5)" if world == 8 else "")
+                                  if world > 1 else ""),
                    "frames_per_gpu": F, "width": W, "height": H, "line_length": ll,
                    "targets": T, "layout": "yuyv", "parallelism": f"dp{world} (frame shards)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
