@@ -25,6 +25,8 @@
 //  * Per tile: DPP wave reduction, one 64-bit atomic per value per wave.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "trik_hsv_internal.h"
 #include "trik_hsv_stripe_px.h"
 
@@ -125,6 +127,7 @@ void stripe_kernel(KernelArgs a, StripeGeom g) {
   const int64_t rowstep = (int64_t)g.k * a.line_length;
   const int col_bytes = LAYOUT == TRIK_HSV_LAYOUT_YUYV ? col * 16 : col * 8;
   const uint32_t x0 = (uint32_t)col * 8;
+  const uint32_t voff = (uint32_t)ro * (uint32_t)a.line_length + (uint32_t)col_bytes;  // < 2^32 (geometry)
 
   const int64_t t_begin = g.n_tiles * blockIdx.x / gridDim.x;
   const int64_t t_end = g.n_tiles * (blockIdx.x + 1) / gridDim.x;
@@ -153,64 +156,78 @@ void stripe_kernel(KernelArgs a, StripeGeom g) {
     // first row) so the compiler can wait with a counted vmcnt.
     const uint8_t* pf = active ? p : a.frames + (int64_t)f * a.frame_stride;
     const int vsteps = active ? min(steps, (a.height - y0 + g.k - 1) / g.k) : 0;  // valid steps, this lane
-    // 4 pixels (words w0, w1) of row y0 + s*k at chunk pixel offset 4*half
-    auto half_step = [&](uint32_t w0, uint32_t w1, int s, int half, uint32_t& Pa, uint32_t& Pb) {
-      const bool valid = s < vsteps;
-      Phase1 p[4];
-      uint32_t m[4], sv[4], e[4];
-      p[0] = phase1<0>(w0, w0 ^ 0xFF00FF00u, m43_lane);
-      p[1] = phase1<1>(w0, w0 ^ 0xFF00FF00u, m43_lane);
-      p[2] = phase1<0>(w1, w1 ^ 0xFF00FF00u, m43_lane);
-      p[3] = phase1<1>(w1, w1 ^ 0xFF00FF00u, m43_lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        m[j] = lds_u32(p[j].m43_addr);
-        sv[j] = lds_u8(p[j].sv_addr);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) e[j] = combine(lds_u32(phase2_addr(m[j], p[j], hue_lane)), sv[j]);
-      if (MASKS && valid) {
-        const int y = y0 + s * g.k;
-        uint8_t* mp = a.masks + ((int64_t)f * a.height + y) * a.width + x0 + 4 * half;
+    // The step loop, in two forms: FULL when every lane of the block is active
+    // and every row of the tile lies in the frame (the common case: no
+    // per-lane validity, a uniform loop counter, loads from a uniform row base
+    // plus a per-lane 32-bit offset); otherwise per-lane row validity.
+    const bool full = (r0 + steps * g.k <= a.height) && (g.k * g.cpr) % 64 == 0;
+    const uint8_t* tbase = a.frames + (int64_t)f * a.frame_stride + (int64_t)r0 * a.line_length;
+    auto run = [&](auto full_c) {
+      constexpr bool FULL = decltype(full_c)::value;
+      // 4 pixels (words w0, w1) of row y0 + s*k at chunk pixel offset 4*half
+      auto half_step = [&](uint32_t w0, uint32_t w1, int s, int half, uint32_t& Pa, uint32_t& Pb) {
+        const bool valid = FULL || s < vsteps;
+        Phase1 p[4];
+        uint32_t m[4], sv[4], e[4];
+        p[0] = phase1<0>(w0, w0 ^ 0xFF00FF00u, m43_lane);
+        p[1] = phase1<1>(w0, w0 ^ 0xFF00FF00u, m43_lane);
+        p[2] = phase1<0>(w1, w1 ^ 0xFF00FF00u, m43_lane);
+        p[3] = phase1<1>(w1, w1 ^ 0xFF00FF00u, m43_lane);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const uint8_t bits = (uint8_t)(pack_bits(e[j]) << a.mask_shift);
-          mp[j] = a.mask_shift ? (uint8_t)(mp[j] | bits) : bits;
+          m[j] = lds_u32(p[j].m43_addr);
+          sv[j] = lds_u8(p[j].sv_addr);
         }
-      }
-      if (valid) {  // false only for rows past the frame end and idle lanes
-        Pa = Pa + e[0] + e[1];
-        Pb = Pb + e[2] + e[3];
-        O = O + e[1] + e[3];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e[j] = combine(lds_u32(phase2_addr(m[j], p[j], hue_lane)), sv[j]);
+        if (MASKS && valid) {
+          const int y = y0 + s * g.k;
+          uint8_t* mp = a.masks + ((int64_t)f * a.height + y) * a.width + x0 + 4 * half;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint8_t bits = (uint8_t)(pack_bits(e[j]) << a.mask_shift);
+            mp[j] = a.mask_shift ? (uint8_t)(mp[j] | bits) : bits;
+          }
+        }
+        if (valid) {  // false only for rows past the frame end and idle lanes
+          Pa = Pa + e[0] + e[1];
+          Pb = Pb + e[2] + e[3];
+          O = O + e[1] + e[3];
+        }
+      };
+      auto step = [&](const uint32_t (&cw)[4], int s) {
+        half_step(cw[0], cw[1], s, 0, P0, P1);
+        half_step(cw[2], cw[3], s, 1, P2, P3);
+        Q = Q + P0 + P1;
+        Q = Q + P2 + P3;
+        ++nb;
+        if (nb == kQFlush || s + 1 == steps) {  // uniform across the block
+          const uint32_t T = Q - (uint32_t)nb * CumS;
+          Qa += T & 0x00FF00FFu;
+          Qb += (T >> 8) & 0x00FF00FFu;
+          Ba += (uint32_t)nb * (CumS & 0x00FF00FFu);
+          Bb += (uint32_t)nb * ((CumS >> 8) & 0x00FF00FFu);
+          CumS = P0 + P1 + P2 + P3;
+          Q = 0;
+          nb = 0;
+        }
+      };
+      auto row_ptr = [&](int s) -> const uint8_t* {
+        if (FULL) return tbase + (int64_t)s * rowstep + voff;
+        return s < vsteps ? pf + (int64_t)s * rowstep : pf;
+      };
+      uint32_t wa[4], wb[4];  // two buffers rotate statically (unroll by 2)
+      load_chunk<LAYOUT>(row_ptr(0), plane, wa);
+      for (int s = 0; s < steps; s += 2) {
+        load_chunk<LAYOUT>(row_ptr(s + 1 < steps || !FULL ? s + 1 : s), plane, wb);
+        step(wa, s);
+        if (s + 1 >= steps) break;
+        load_chunk<LAYOUT>(row_ptr(s + 2 < steps || !FULL ? s + 2 : s), plane, wa);
+        step(wb, s + 1);
       }
     };
-    auto step = [&](const uint32_t (&cw)[4], int s) {
-      half_step(cw[0], cw[1], s, 0, P0, P1);
-      half_step(cw[2], cw[3], s, 1, P2, P3);
-      Q = Q + P0 + P1;
-      Q = Q + P2 + P3;
-      ++nb;
-      if (nb == kQFlush || s + 1 == steps) {  // uniform across the block
-        const uint32_t T = Q - (uint32_t)nb * CumS;
-        Qa += T & 0x00FF00FFu;
-        Qb += (T >> 8) & 0x00FF00FFu;
-        Ba += (uint32_t)nb * (CumS & 0x00FF00FFu);
-        Bb += (uint32_t)nb * ((CumS >> 8) & 0x00FF00FFu);
-        CumS = P0 + P1 + P2 + P3;
-        Q = 0;
-        nb = 0;
-      }
-    };
-    auto row_ptr = [&](int s) { return s < vsteps ? pf + (int64_t)s * rowstep : pf; };
-    uint32_t wa[4], wb[4];  // two buffers rotate statically (unroll by 2)
-    load_chunk<LAYOUT>(row_ptr(0), plane, wa);
-    for (int s = 0; s < steps; s += 2) {
-      load_chunk<LAYOUT>(row_ptr(s + 1), plane, wb);
-      step(wa, s);
-      if (s + 1 >= steps) break;
-      load_chunk<LAYOUT>(row_ptr(s + 2), plane, wa);
-      step(wb, s + 1);
-    }
+    if (full) run(std::true_type{});
+    else run(std::false_type{});
     Qa += Ba;  // sum over steps of the cumulative count, 16-bit fields
     Qb += Bb;
 
