@@ -37,7 +37,7 @@ namespace {
 using namespace stripe_px;
 
 constexpr int kMaxBlock = 1024;
-constexpr int kMaxSteps = 31;  // byte counters: P_i <= 2*31, sum of four <= 248
+constexpr int kMaxSteps = 63;  // byte counters: P_i <= 2*63, O <= 4*63 (a VGA frame is one 40-step tile)
 constexpr int kQFlush = 7;     // steps per Q block: block-relative sums <= 8*(1+...+7) = 224
 
 struct StripeGeom {
@@ -147,8 +147,10 @@ void stripe_kernel(KernelArgs a, StripeGeom g) {
     //         Q - nb*CumS has true fields in [0, 224], and packed arithmetic
     //         is exact mod 2^32, so the fields come out right.
     //   Qa/Qb, Ba/Bb : 16-bit fields (ranges 0,2 / 1,3) collecting, per block,
-    //         the sums above and nb*CumS.
-    uint32_t P0 = 0, P1 = 0, P2 = 0, P3 = 0, O = 0, Q = 0, CumS = 0;
+    //         the sums above and nb*CumS.  CumS's byte fields may exceed 255
+    //         past 31 steps (it only enters mod-2^32 linear terms); CumA/CumB
+    //         hold the same counts in 16-bit fields for Ba/Bb and the totals.
+    uint32_t P0 = 0, P1 = 0, P2 = 0, P3 = 0, O = 0, Q = 0, CumS = 0, CumA = 0, CumB = 0;
     uint32_t Qa = 0, Qb = 0, Ba = 0, Bb = 0;
     int nb = 0;
     // Software pipeline, one row ahead (8 waves per SIMD hide the rest).
@@ -205,9 +207,12 @@ void stripe_kernel(KernelArgs a, StripeGeom g) {
           const uint32_t T = Q - (uint32_t)nb * CumS;
           Qa += T & 0x00FF00FFu;
           Qb += (T >> 8) & 0x00FF00FFu;
-          Ba += (uint32_t)nb * (CumS & 0x00FF00FFu);
-          Bb += (uint32_t)nb * ((CumS >> 8) & 0x00FF00FFu);
+          Ba += (uint32_t)nb * CumA;
+          Bb += (uint32_t)nb * CumB;
           CumS = P0 + P1 + P2 + P3;
+          CumA = (P0 & 0x00FF00FFu) + (P1 & 0x00FF00FFu) + (P2 & 0x00FF00FFu) + (P3 & 0x00FF00FFu);
+          CumB = ((P0 >> 8) & 0x00FF00FFu) + ((P1 >> 8) & 0x00FF00FFu) + ((P2 >> 8) & 0x00FF00FFu) +
+                 ((P3 >> 8) & 0x00FF00FFu);
           Q = 0;
           nb = 0;
         }
@@ -233,11 +238,11 @@ void stripe_kernel(KernelArgs a, StripeGeom g) {
 
     // unpack per range, wave-reduce, one atomic per value per wave and tile
     uint32_t acc[3 * NR];
-    const uint32_t C = P0 + P1 + P2 + P3;
+    // the last step always flushed, so CumA/CumB hold the tile's counts
 #pragma unroll
     for (int rr = 0; rr < NR; ++rr) {
       const int sh = 8 * rr;
-      const uint32_t c = (C >> sh) & 0xFFu;
+      const uint32_t c = ((rr & 1) ? (CumB >> ((rr >> 1) * 16)) : (CumA >> ((rr >> 1) * 16))) & 0xFFFFu;
       const uint32_t wx = 2u * ((P1 >> sh) & 0xFFu) + 4u * ((P2 >> sh) & 0xFFu) +
                           6u * ((P3 >> sh) & 0xFFu) + ((O >> sh) & 0xFFu);
       const uint32_t qq = ((rr & 1) ? (Qb >> ((rr >> 1) * 16)) : (Qa >> ((rr >> 1) * 16))) & 0xFFFFu;
