@@ -81,3 +81,17 @@ def test_batch_api_on_a_side_stream(hsv, oracle_mod):
         assert np.array_equal(targets[:, :, :3].cpu().numpy(), want_t)
     finally:
         det.close()
+
+
+def test_import_order_one_hip_runtime(hsv):
+    """`import trik_hsv` before `import torch` in a fresh interpreter: the
+    package binds the library to torch's HIP runtime."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r); import trik_hsv; import torch; "
+            "d = trik_hsv.Detector(); d.close(); print('ok')" % os.path.join(root, "trik-media-sensors-dsp_amd"))
+    res = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0 and "ok" in res.stdout, res.stderr[-2000:]

@@ -217,17 +217,22 @@ void stripe_kernel(KernelArgs a, StripeGeom g) {
           nb = 0;
         }
       };
+      // FULL: a uniform row base advanced by rowstep per step (scalar adds),
+      // plus the lane's 32-bit offset
+      const uint8_t* rb = tbase;
       auto row_ptr = [&](int s) -> const uint8_t* {
-        if (FULL) return tbase + (int64_t)s * rowstep + voff;
+        if (FULL) return rb + voff;
         return s < vsteps ? pf + (int64_t)s * rowstep : pf;
       };
       uint32_t wa[4], wb[4];  // two buffers rotate statically (unroll by 2)
       load_chunk<LAYOUT>(row_ptr(0), plane, wa);
       for (int s = 0; s < steps; s += 2) {
-        load_chunk<LAYOUT>(row_ptr(s + 1 < steps || !FULL ? s + 1 : s), plane, wb);
+        if (FULL && s + 1 < steps) rb += rowstep;
+        load_chunk<LAYOUT>(row_ptr(s + 1), plane, wb);
         step(wa, s);
         if (s + 1 >= steps) break;
-        load_chunk<LAYOUT>(row_ptr(s + 2 < steps || !FULL ? s + 2 : s), plane, wa);
+        if (FULL && s + 2 < steps) rb += rowstep;
+        load_chunk<LAYOUT>(row_ptr(s + 2), plane, wa);
         step(wb, s + 1);
       }
     };

@@ -207,6 +207,15 @@ def load() -> C.CDLL:
     """Load libtrik_hsv.so; raises if it has not been built (no fallback)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64 /
+        # libhsa-runtime64 (same SONAME, loaded by path).  If this library loaded
+        # /opt/rocm's first, importing torch afterwards would map a second HSA
+        # runtime and this library's would see no device.  Loading torch first
+        # makes the library's DT_NEEDED libamdhip64.so.7 bind to torch's copy.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is missing: build it with `make -C {CSRC}` "
                               "(or __graft_entry__.build()); there is no CPU fallback")
