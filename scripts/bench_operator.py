@@ -72,7 +72,7 @@ def main():
                       "bytes_algorithmic": pv_bytes,
                       "achieved_GBs": round(pv_bytes / (pv_ms / 1e3) / 1e9, 1),
                       "hbm_frac": round(pv_bytes / (pv_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                      "note": "preview_kernel (writes every preview byte) + overlay_kernel"}
+                      "note": "preview_gather_kernel (writes every preview byte) + overlay_kernel"}
 
     ar_ms = timed(lambda: trik_hsv.batch_auto_range(dev, W, H, LL, trik_hsv.LAYOUT_YUYV), stream,
                   args.iters)

@@ -123,6 +123,29 @@ def test_batch_auto_range(hsv, oracle_mod, w, h, ll, layout, kind):
                                    want["detect_val_tol"]], f
 
 
+@pytest.mark.parametrize("layout", [LAYOUT_YUYV, LAYOUT_OV7670])
+def test_batch_auto_range_large_batch(hsv, oracle_mod, layout):
+    """>= 512 frames take the two-pass kernel, fewer the one-pass kernel
+    (operator.hip:launch_auto_range): both = the oracle, frame by frame."""
+    import torch
+
+    w, h, n = 160, 120, 520
+    ll = 2 * w if layout == LAYOUT_YUYV else w
+    fb = hsv.frame_bytes(w, h, ll, layout)
+    dev = torch.empty(n * fb, dtype=torch.uint8, device="cuda")
+    hsv.synth(dev, w, h, ll, layout, 1, SEED + 7, first_frame=3)
+    got = hsv.batch_auto_range(dev, w, h, ll, layout).cpu().numpy().astype(np.int64)
+    few = hsv.batch_auto_range(dev[:16 * fb], w, h, ll, layout).cpu().numpy().astype(np.int64)
+    assert np.array_equal(got[:16], few)
+    host = dev.cpu().numpy()
+    for f in range(n):
+        _, want, _ = oracle_mod.run(host[f * fb:(f + 1) * fb], w, h, ll, layout, T0,
+                                    auto_detect=True, preview=False)
+        assert got[f].tolist() == [want["detect_hue"], want["detect_hue_tol"], want["detect_sat"],
+                                   want["detect_sat_tol"], want["detect_val"],
+                                   want["detect_val_tol"]], f
+
+
 @pytest.mark.parametrize("w,h,ll,ow,oh,oll,layout,kind", [
     (640, 480, 1280, 320, 240, 640, LAYOUT_YUYV, 1),
     (640, 480, 1280, 320, 240, 640, LAYOUT_YUYV, 0),

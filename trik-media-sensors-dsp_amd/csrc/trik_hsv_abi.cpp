@@ -521,6 +521,8 @@ AutoRangeArgs auto_range_args(const TrikHsvFrameBatch& b, uint16_t* out) {
   a.n_frames = b.n_frames;
   a.width = b.width; a.height = b.height; a.line_length = b.line_length; a.layout = b.layout;
   auto_range_zone(b.width, b.height, a.c_lo, a.c_hi, a.r_lo, a.r_hi);
+  a.aligned4 = (reinterpret_cast<uintptr_t>(b.frames) & 3) == 0 && (b.n_frames <= 1 || (b.frame_stride & 3) == 0) &&
+               (b.line_length & 3) == 0;
   a.out = out;
   return a;
 }

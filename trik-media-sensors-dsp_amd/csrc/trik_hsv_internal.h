@@ -101,6 +101,7 @@ struct AutoRangeArgs {
   int64_t frame_stride;
   int32_t n_frames, width, height, line_length, layout;
   int32_t c_lo, c_hi, r_lo, r_hi;  // exclusive zone bounds (uint16 values, hpp:88-108)
+  int32_t aligned4;                // frames, stride and line length 4-byte aligned
   uint16_t* out;
 };
 

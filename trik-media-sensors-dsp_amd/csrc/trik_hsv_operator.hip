@@ -157,73 +157,116 @@ __global__ __launch_bounds__(64) void overlay_kernel(PreviewArgs a, const TrikHs
 
 constexpr int kRangeBlock = 256;
 
-// H, S, V bytes of one pixel (WSEQ:207-249) from the constant LUTs.
+// H, S, V bytes of one pixel (WSEQ:207-249), branch-free as the hot kernel's
+// phase1 (clamp8_shift6 on v_dot4 presums, the hue case as selects), with
+// LUT43 / LUT255 in LDS.
 __device__ __forceinline__ void hsv_bytes(const uint8_t* fr, const AutoRangeArgs& a, int row, int col,
-                                          uint32_t (&hsv)[3]) {
-  int Y, U, V;
-  fetch_yuv(fr, a.height, a.line_length, a.layout, row, col, Y, U, V);
-  const PixelRgb p = pixel_rgb(Y, U, V);
-  const int mx = max(p.r, max(p.g, p.b)), mn = min(p.r, min(p.g, p.b));
-  const int m = c_luts.l43[mx - mn];
-  int h;
-  if (mx == p.g) h = 21845 + m * (p.b - p.r);
-  else if (mx == p.b) h = 43690 + m * (p.r - p.g);
-  else h = m * (p.g - p.b);
+                                          const uint16_t* l43, const uint16_t* l255, uint32_t (&hsv)[3]) {
+  using stripe_px::clamp8_shift6;
+  uint32_t w;  // the pixel as a YUYV word with its Y in byte 0
+  if (a.layout == TRIK_HSV_LAYOUT_YUYV && a.aligned4) {
+    w = *reinterpret_cast<const uint32_t*>(fr + (int64_t)row * a.line_length + 4 * (col >> 1));
+    if (col & 1) w = __builtin_amdgcn_perm(w, w, 0x03020102u);
+  } else {
+    int Y, U, V;
+    fetch_yuv(fr, a.height, a.line_length, a.layout, row, col, Y, U, V);
+    w = (uint32_t)Y | ((uint32_t)U << 8) | ((uint32_t)V << 24);
+  }
+  const uint32_t wc = w ^ 0xFF00FF00u;
+  const int r = clamp8_shift6(__builtin_amdgcn_udot4(w, 74u | (102u << 24), (uint32_t)-14248, false));
+  const int g = clamp8_shift6(__builtin_amdgcn_udot4(wc, 74u | (25u << 8) | (52u << 24), (uint32_t)-10939, false));
+  const int b = clamp8_shift6(__builtin_amdgcn_udot4(w, 74u | (129u << 8), (uint32_t)-17672, false));
+  const int mx = max(r, max(g, b)), mn = min(r, min(g, b));
+  const bool eqG = mx == g, eqB = mx == b;  // priority G > B > R (WSEQ:226-246)
+  const int diff = eqG ? b - r : (eqB ? r - g : g - b);
+  const int base = eqG ? 21845 : (eqB ? 43690 : 0);
+  const int h = base + (int)l43[mx - mn] * diff;
   hsv[0] = ((uint32_t)h >> 8) & 0xFFu;
-  hsv[1] = ((uint32_t)c_luts.l255[mx] * (uint32_t)(mx - mn)) >> 8;
+  hsv[1] = ((uint32_t)l255[mx] * (uint32_t)(mx - mn)) >> 8;
   hsv[2] = (uint32_t)mx;
 }
 
+// Per-wave sub-histograms (same-bin LDS atomics contend only within a wave).
+// kTwoPass = false: one pass records counts and last positions per value.
+// kTwoPass = true: pass 1 counts; pass 2 records the last position of the
+// values whose count is the maximum M only (the other pixels do no atomic) --
+// fewer LDS atomics, two reads of the zone: faster when the batch fills the
+// chip, slower for a single frame (one workgroup, latency-bound).  Either way
+// the winner is, among the values with count M, the one with the earliest
+// last occurrence (see the file comment).
+template <bool kTwoPass>
 __global__ __launch_bounds__(kRangeBlock) void auto_range_kernel(AutoRangeArgs a) {
-  __shared__ uint32_t cnt[3][256];
-  __shared__ uint32_t last[3][256];
+  constexpr int kWaves = kRangeBlock / 64;
+  constexpr int kLastSets = kTwoPass ? 1 : kWaves;
+  __shared__ uint32_t cnt[kWaves][3][256];
+  __shared__ uint32_t lst[kLastSets][3][256];
+  __shared__ uint32_t best_n[3];
   __shared__ uint64_t best[3];
-  const int f = blockIdx.x;
-  for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) {
-    (&cnt[0][0])[i] = 0;
-    (&last[0][0])[i] = 0;
+  __shared__ uint16_t l43[256], l255[256];
+  const int f = blockIdx.x, tid = threadIdx.x, wave = tid >> 6;
+  for (int i = tid; i < kWaves * 3 * 256; i += blockDim.x) (&cnt[0][0][0])[i] = 0;
+  for (int i = tid; i < kLastSets * 3 * 256; i += blockDim.x) (&lst[0][0][0])[i] = 0;
+  for (int i = tid; i < 256; i += blockDim.x) {
+    l43[i] = c_luts.l43[i];
+    l255[i] = c_luts.l255[i];
   }
-  if (threadIdx.x < 3) best[threadIdx.x] = ~0ull;
+  if (tid < 3) {
+    best_n[tid] = 0;
+    best[tid] = ~0ull;
+  }
   __syncthreads();
   // zone: c_lo < col < c_hi, r_lo < row < r_hi (uint16 bounds, hpp:88-108)
   const int c0 = max(a.c_lo + 1, 0), c1 = min(a.c_hi, a.width);  // [c0, c1)
   const int r0 = max(a.r_lo + 1, 0), r1 = min(a.r_hi, a.height);
   const int zw = c1 - c0, zh = r1 - r0;
+  const int64_t zn = zw > 0 && zh > 0 ? (int64_t)zw * zh : 0;
   const uint8_t* fr = a.frames + (int64_t)f * a.frame_stride;
-  if (zw > 0 && zh > 0) {
-    for (int64_t i = threadIdx.x; i < (int64_t)zw * zh; i += blockDim.x) {
+  for (int64_t i = tid; i < zn; i += blockDim.x) {
+    const int row = r0 + (int)(i / zw), col = c0 + (int)(i % zw);
+    uint32_t hv[3];
+    hsv_bytes(fr, a, row, col, l43, l255, hv);
+    const uint32_t pos = (uint32_t)((int64_t)row * a.width + col);  // scan order of s_rgb888hsv
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      atomicAdd(&cnt[wave][k][hv[k]], 1u);
+      if (!kTwoPass) atomicMax(&lst[kTwoPass ? 0 : wave][k][hv[k]], pos);
+    }
+  }
+  __syncthreads();
+  // merge the waves: counts add, last positions take the maximum
+  for (int i = tid; i < 3 * 256; i += blockDim.x) {
+    uint32_t n = 0, l = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) n += (&cnt[w][0][0])[i];
+#pragma unroll
+    for (int w = 0; w < kLastSets; ++w) l = max(l, (&lst[w][0][0])[i]);
+    (&cnt[0][0][0])[i] = n;
+    (&lst[0][0][0])[i] = l;
+    if (n) atomicMax(&best_n[i >> 8], n);
+  }
+  __syncthreads();
+  if (kTwoPass) {
+    for (int64_t i = tid; i < zn; i += blockDim.x) {
       const int row = r0 + (int)(i / zw), col = c0 + (int)(i % zw);
       uint32_t hv[3];
-      hsv_bytes(fr, a, row, col, hv);
-      const uint32_t pos = (uint32_t)((int64_t)row * a.width + col);  // scan order of s_rgb888hsv
+      hsv_bytes(fr, a, row, col, l43, l255, hv);
+      const uint32_t pos = (uint32_t)((int64_t)row * a.width + col);
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        atomicAdd(&cnt[k][hv[k]], 1u);
-        atomicMax(&last[k][hv[k]], pos);
-      }
+      for (int k = 0; k < 3; ++k)
+        if (cnt[0][k][hv[k]] == best_n[k]) atomicMax(&lst[0][k][hv[k]], pos);
     }
+    __syncthreads();
   }
-  __syncthreads();
-  // per channel: max count M, then the earliest last occurrence among count == M
-  // key = (~count) << 32 | last  ->  min key = max count, then min last
-  for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) {
+  for (int i = tid; i < 3 * 256; i += blockDim.x) {
     const int k = i >> 8, v = i & 255;
-    const uint32_t c = cnt[k][v];
-    if (c) atomicMin(reinterpret_cast<unsigned long long*>(&best[k]),
-                     ((unsigned long long)(~c) << 32) | last[k][v]);
+    const uint32_t n = cnt[0][k][v];
+    if (n && n == best_n[k])
+      atomicMin(reinterpret_cast<unsigned long long*>(&best[k]), ((unsigned long long)lst[0][k][v] << 8) | (unsigned)v);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (tid == 0) {
     uint32_t win[3];
-    for (int k = 0; k < 3; ++k) {
-      win[k] = 0;  // no zone pixels: the reference keeps m_max* = 0
-      if (best[k] != ~0ull) {
-        const uint32_t pos = (uint32_t)best[k];
-        uint32_t hv[3];  // the winning value is the one at its last position
-        hsv_bytes(fr, a, (int)(pos / (uint32_t)a.width), (int)(pos % (uint32_t)a.width), hv);
-        win[k] = hv[k];
-      }
-    }
+    for (int k = 0; k < 3; ++k) win[k] = best[k] != ~0ull ? (uint32_t)(best[k] & 0xFFu) : 0u;  // none: m_max* = 0
     uint16_t* o = a.out + (int64_t)f * 6;  // hpp:190-195: float constants promoted to double
     o[0] = (uint16_t)((double)win[0] * (double)1.4f);
     o[1] = 15;
@@ -279,7 +322,11 @@ int launch_preview(const PreviewArgs& a, const TrikHsvTargetSums* sums, int sums
 
 int launch_auto_range(const AutoRangeArgs& a, hipStream_t s) {
   if (a.n_frames <= 0) return hipSuccess;
-  hipLaunchKernelGGL(auto_range_kernel, dim3((unsigned)a.n_frames), dim3(kRangeBlock), 0, s, a);
+  // one workgroup per frame; two passes once the batch fills the chip (2 per CU)
+  if (a.n_frames >= 512)
+    hipLaunchKernelGGL(auto_range_kernel<true>, dim3((unsigned)a.n_frames), dim3(kRangeBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL(auto_range_kernel<false>, dim3((unsigned)a.n_frames), dim3(kRangeBlock), 0, s, a);
   return hipGetLastError();
 }
 
