@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=512, help="CPU baseline sample (frames)")
     ap.add_argument("--cpu-frames-1core", type=int, default=32, help="single-thread CPU sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--hot", choices=["auto", "stripe", "chroma"], default="auto",
+                    help="hot kernel (auto = the library's choice: chroma-run for this batch size)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="rocprofv3 FETCH_SIZE summary used for roofline.traffic")
     return ap.parse_args()
@@ -136,6 +138,8 @@ def main():
     assert count == F
     trik_hsv.synth(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, args.kind, SEED, first_frame=first)
     det = trik_hsv.Detector()
+    trik_hsv.set_hot_kernel({"auto": trik_hsv.HOT_AUTO, "stripe": trik_hsv.HOT_STRIPE,
+                             "chroma": trik_hsv.HOT_CHROMA}[args.hot])
     sums = torch.zeros((F, T, 3), dtype=torch.int64, device=dev)
 
     def step(ev0=None, ev1=None):
@@ -165,6 +169,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    kname = {trik_hsv.HOT_CHROMA: "chroma_kernel", trik_hsv.HOT_STRIPE: "stripe_kernel",
+             trik_hsv.HOT_GENERIC: "reduce_kernel"}.get(trik_hsv.last_hot_kernel(), "?")
 
     el = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:
@@ -190,7 +196,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": load_traffic(args.pmc, bytes_per_launch),
-                     "kernel": "stripe_kernel<YUYV,4>", "kernel_ms": round(kern_ms, 4),
+                     "kernel": f"{kname}<YUYV,{T}>", "kernel_ms": round(kern_ms, 4),
                      "kernel_ms_max_rank": round(kern_ms_max, 4),
                      "bytes_per_launch": bytes_per_launch},
     }

@@ -386,6 +386,21 @@ int32_t trik_hsv_batch_sums(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvFra
                             const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int32_t n_ranges,
                             TrikHsvTargetSums* sums_dev, void* hip_stream);
 
+/* Hot-kernel selection for trik_hsv_batch_sums / _process_batch / _masks
+ * (process-wide; for tests and A/B runs).  TRIK_HSV_HOT_AUTO picks the
+ * chroma-run kernel for batches of at least TRIK_HSV_CHROMA_MIN_PIXELS pixels
+ * whose geometry it takes, the stripe kernel otherwise; the two give the same
+ * results.  Returns the previous setting, or -1 for an unknown kind. */
+#define TRIK_HSV_HOT_AUTO 0
+#define TRIK_HSV_HOT_STRIPE 1
+#define TRIK_HSV_HOT_CHROMA 2
+#define TRIK_HSV_HOT_GENERIC 3
+#define TRIK_HSV_CHROMA_MIN_PIXELS (32 * 640 * 480)
+int32_t trik_hsv_set_hot_kernel(int32_t kind);
+/* The kernel the last hot launch on this thread ran (TRIK_HSV_HOT_STRIPE,
+ * _CHROMA or _GENERIC; 0 before any). */
+int32_t trik_hsv_last_hot_kernel(void);
+
 /* Epilogue only: sums_dev -> targets_dev for an n_frames x n_ranges grid. */
 int32_t trik_hsv_batch_targets(const TrikHsvFrameBatch* batch, int32_t n_ranges,
                                const TrikHsvTargetSums* sums_dev, TrikHsvTarget* targets_dev,

@@ -1,0 +1,187 @@
+"""GPU parity of the chroma-run hot kernel (trik_hsv_chroma.hip) against the
+CPU oracle, bit-exact, through the C ABI with the kernel forced by
+trik_hsv.set_hot_kernel(HOT_CHROMA).
+
+The kernel resolves most YUYV words from per-chroma run descriptors and the
+rest ("exception" chromas, ~12 % at the bench's 4 ranges) from exact profile
+rows, so the cases below cover both paths: every (Y,U,V) triple, uniform and
+scene batches at the configs' shapes, several range groups, strided and
+padded frames, and the table rebuild when the range set changes.
+"""
+import numpy as np
+import pytest
+
+from gpu_util import (BENCH_RANGES, LAYOUT_OV7670, LAYOUT_YUYV, T0, T1,
+                      exhaustive_yuyv_frame, sums_from_mask)
+from test_gpu_parity import EDGE_RANGES
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def hsv():
+    import trik_hsv
+
+    return trik_hsv
+
+
+@pytest.fixture(scope="module")
+def detector(hsv, torch_dev):
+    d = hsv.Detector()
+    yield d
+    d.close()
+
+
+@pytest.fixture()
+def chroma(hsv):
+    prev = hsv.set_hot_kernel(hsv.HOT_CHROMA)
+    yield hsv
+    hsv.set_hot_kernel(prev)
+
+
+def _to_dev(torch, arr):
+    return torch.from_numpy(np.ascontiguousarray(arr)).cuda()
+
+
+@pytest.mark.parametrize("group", ["bench", "edge"])
+def test_chroma_exhaustive_all_yuv_triples(torch_dev, detector, oracle_mod, chroma, group):
+    """Every (Y,U,V) triple (verification mode writes each pixel's mask, from
+    the run descriptor or the exception row) vs the oracle."""
+    torch = torch_dev
+    ranges = BENCH_RANGES + EDGE_RANGES[:4] if group == "bench" else EDGE_RANGES
+    frame, w, h, ll = exhaustive_yuyv_frame()
+    _, want = oracle_mod.frame(frame, w, h, ll, LAYOUT_YUYV, ranges, want_mask=True)
+    masks, sums = detector.batch_masks(_to_dev(torch, frame), w, h, ll, LAYOUT_YUYV, ranges)
+    assert chroma.last_hot_kernel() == chroma.HOT_CHROMA
+    got = masks[0].cpu().numpy()
+    bad = np.count_nonzero(got != want)
+    assert bad == 0, f"{bad} pixels differ; first at {np.argwhere(got != want)[:5].tolist()}"
+    assert sums[0].cpu().numpy().tolist() == sums_from_mask(want, len(ranges)).tolist()
+
+
+def test_chroma_exhaustive_ov7670(torch_dev, detector, oracle_mod, chroma):
+    torch = torch_dev
+    frame, w, h, ll = exhaustive_yuyv_frame()
+    px = frame.reshape(h, w // 2, 4)
+    ylum = np.stack([px[..., 0], px[..., 2]], -1).reshape(h, w)
+    chrom = np.stack([px[..., 3], px[..., 1]], -1).reshape(h, w)  # even = V, odd = U
+    planar = np.concatenate([ylum.reshape(-1), chrom.reshape(-1)])
+    _, want = oracle_mod.frame(planar, w, h, w, LAYOUT_OV7670, BENCH_RANGES, want_mask=True)
+    masks, sums = detector.batch_masks(_to_dev(torch, planar), w, h, w, LAYOUT_OV7670, BENCH_RANGES)
+    assert chroma.last_hot_kernel() == chroma.HOT_CHROMA
+    assert np.array_equal(masks[0].cpu().numpy(), want)
+    assert sums[0].cpu().numpy().tolist() == sums_from_mask(want, 4).tolist()
+
+
+@pytest.mark.parametrize("w,h,layout,kind,ranges,n", [
+    (640, 480, LAYOUT_YUYV, 0, BENCH_RANGES, 24),          # C3 shape, uniform (12 % exceptions)
+    (640, 480, LAYOUT_YUYV, 1, BENCH_RANGES, 24),          # C3 shape, scene
+    (1280, 720, LAYOUT_YUYV, 0, [T0, T1], 8),              # C4 shape, uniform
+    (1280, 720, LAYOUT_YUYV, 1, [T0, T1], 8),              # C4 shape, scene
+    (320, 240, LAYOUT_OV7670, 0, [T0], 16),                # C1 layout
+    (640, 480, LAYOUT_YUYV, 0, [T0], 3),                   # C2 shape
+    (640, 480, LAYOUT_YUYV, 0, BENCH_RANGES + EDGE_RANGES, 4),  # 12 ranges = 3 launches
+    (8192, 8, LAYOUT_YUYV, 0, BENCH_RANGES, 6),            # widest row, 3 drain rounds per unpack
+    (32, 4, LAYOUT_YUYV, 0, BENCH_RANGES, 40),             # minimal frame, 31 rows per step
+    (64, 1000, LAYOUT_OV7670, 0, BENCH_RANGES[:3], 3),     # tall: several tiles per frame
+])
+def test_chroma_batch_vs_oracle(torch_dev, hsv, detector, oracle_mod, chroma, w, h, layout, kind, ranges, n):
+    torch = torch_dev
+    ll = 2 * w if layout == LAYOUT_YUYV else w
+    fb = hsv.frame_bytes(w, h, ll, layout)
+    dev = torch.empty(n * fb, dtype=torch.uint8, device="cuda")
+    hsv.synth(dev, w, h, ll, layout, kind, 0x7A1C, first_frame=100)
+    host = oracle_mod.synth(n, w, h, ll, layout, kind, 0x7A1C, first_frame=100)
+    assert np.array_equal(dev.cpu().numpy(), host)
+    sums, tg = detector.process_batch(dev, w, h, ll, layout, ranges)
+    assert hsv.last_hot_kernel() == hsv.HOT_CHROMA
+    want_s, want_t = oracle_mod.batch(host, fb, n, w, h, ll, layout, ranges, n_threads=8)
+    assert np.array_equal(sums.cpu().numpy(), want_s)
+    assert np.array_equal(tg[:, :, :3].cpu().numpy(), want_t)
+
+
+def test_chroma_padded_and_strided(torch_dev, hsv, detector, oracle_mod, chroma):
+    """lineLength padding and a frame stride past the frame (16-byte aligned:
+    the chroma kernel's vector loads); a misaligned base falls back."""
+    torch = torch_dev
+    for (w, h, ll, lay) in [(64, 8, 160, LAYOUT_YUYV), (96, 12, 112, LAYOUT_OV7670),
+                            (640, 480, 1344, LAYOUT_YUYV)]:
+        fb = hsv.frame_bytes(w, h, ll, lay)
+        stride = (fb + 48 + 15) // 16 * 16
+        n = 5
+        host = oracle_mod.synth(n, w, h, ll, lay, 0, 42, frame_stride=stride)
+        ranges = BENCH_RANGES + EDGE_RANGES[:2]
+        sums, tg = detector.process_batch(_to_dev(torch, host), w, h, ll, lay, ranges, n_frames=n,
+                                          frame_stride=stride)
+        assert hsv.last_hot_kernel() == hsv.HOT_CHROMA, (w, h, ll, lay)
+        want_s, want_t = oracle_mod.batch(host, stride, n, w, h, ll, lay, ranges)
+        assert np.array_equal(sums.cpu().numpy(), want_s), (w, h, ll, lay)
+        assert np.array_equal(tg[:, :, :3].cpu().numpy(), want_t), (w, h, ll, lay)
+    # a misaligned base cannot take the vector loads: the generic kernel runs
+    w, h, ll = 64, 8, 160
+    host = oracle_mod.synth(2, w, h, ll, LAYOUT_YUYV, 0, 42)
+    buf = np.zeros(host.size + 1, np.uint8)
+    buf[1:] = host
+    sums, _ = detector.process_batch(_to_dev(torch, buf)[1:], w, h, ll, LAYOUT_YUYV, [T0], n_frames=2)
+    assert hsv.last_hot_kernel() == hsv.HOT_GENERIC
+    want_s, _ = oracle_mod.batch(host, h * ll, 2, w, h, ll, LAYOUT_YUYV, [T0])
+    assert np.array_equal(sums.cpu().numpy(), want_s)
+
+
+def test_chroma_range_set_changes(torch_dev, hsv, detector, oracle_mod, chroma):
+    """The chroma tables are rebuilt when the range set changes (and reused
+    when it comes back)."""
+    torch = torch_dev
+    w, h, ll, n = 640, 480, 1280, 6
+    dev = torch.empty(n * h * ll, dtype=torch.uint8, device="cuda")
+    hsv.synth(dev, w, h, ll, LAYOUT_YUYV, 0, 7)
+    host = dev.cpu().numpy()
+    for ranges in (BENCH_RANGES, [EDGE_RANGES[3], T1], BENCH_RANGES, EDGE_RANGES[4:]):
+        sums, _ = detector.process_batch(dev, w, h, ll, LAYOUT_YUYV, ranges)
+        want, _ = oracle_mod.batch(host, h * ll, n, w, h, ll, LAYOUT_YUYV, ranges, n_threads=8)
+        assert np.array_equal(sums.cpu().numpy(), want), ranges
+
+
+def test_chroma_equals_stripe_on_full_c3(torch_dev, hsv, detector, oracle_mod):
+    """The bench workload (4096 x 640x480, T=4): AUTO picks the chroma kernel,
+    its sums equal the stripe kernel's for every frame, and sampled frames
+    equal the oracle."""
+    torch = torch_dev
+    w, h, ll, n = 640, 480, 1280, 4096
+    dev = torch.empty(n * h * ll, dtype=torch.uint8, device="cuda")
+    hsv.synth(dev, w, h, ll, LAYOUT_YUYV, 0, 0x7A1C)
+    prev = hsv.set_hot_kernel(hsv.HOT_AUTO)
+    try:
+        s_auto, t_auto = detector.process_batch(dev, w, h, ll, LAYOUT_YUYV, BENCH_RANGES)
+        assert hsv.last_hot_kernel() == hsv.HOT_CHROMA
+        hsv.set_hot_kernel(hsv.HOT_STRIPE)
+        s_str, t_str = detector.process_batch(dev, w, h, ll, LAYOUT_YUYV, BENCH_RANGES)
+        assert hsv.last_hot_kernel() == hsv.HOT_STRIPE
+    finally:
+        hsv.set_hot_kernel(prev)
+    assert torch.equal(s_auto, s_str) and torch.equal(t_auto, t_str)
+    s = s_auto.cpu().numpy()
+    for f in (0, 1, 2047, 4095):
+        host = oracle_mod.synth(1, w, h, ll, LAYOUT_YUYV, 0, 0x7A1C, first_frame=f)
+        want, _ = oracle_mod.frame(host, w, h, ll, LAYOUT_YUYV, BENCH_RANGES)
+        assert np.array_equal(s[f], want), f
+
+
+def test_auto_keeps_small_batches_on_stripe(torch_dev, hsv, detector):
+    torch = torch_dev
+    dev = torch.zeros(4 * 480 * 1280, dtype=torch.uint8, device="cuda")
+    prev = hsv.set_hot_kernel(hsv.HOT_AUTO)
+    try:
+        detector.process_batch(dev, 640, 480, 1280, LAYOUT_YUYV, [T0])
+        assert hsv.last_hot_kernel() == hsv.HOT_STRIPE
+    finally:
+        hsv.set_hot_kernel(prev)

@@ -7,6 +7,7 @@
 // pointers in process-wide statics, WSEQ:23-26,63-64) and the pixel work on
 // the GPU.  Layer 2 (trik_hsv_*) is the batched device API the GPU work sits
 // behind.  No C++ exception escapes any entry point.
+#include <atomic>
 #include <hip/hip_runtime.h>
 #include <limits.h>
 #include <string.h>
@@ -135,7 +136,12 @@ struct TableSet {
   RangeTables* h_tables = nullptr;
   StripeTables* d_stripe = nullptr;
   StripeTables* h_stripe = nullptr;
+  ChromaTables* d_chroma = nullptr;  // built on first use per range set (chroma-run kernel)
+  bool chroma_built = false;
   void release() {
+    (void)hipFree(d_chroma);
+    d_chroma = nullptr;
+    chroma_built = false;
     (void)hipFree(d_tables);
     (void)hipHostFree(h_tables);
     (void)hipFree(d_stripe);
@@ -310,8 +316,22 @@ int32_t ensure_tables(TrikCvHandle* h, TableSet& t, const TRIK_VIDTRANSCODE_CV_I
   HIP_TRY(hipMemcpyAsync(t.d_tables, t.h_tables, sizeof(RangeTables) * groups, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(t.d_stripe, t.h_stripe, sizeof(StripeTables) * groups, hipMemcpyHostToDevice, s));
   t.key.swap(key);
+  t.chroma_built = false;
   return 0;
 }
+
+// The chroma-run kernel's tables for the current range set (built on the
+// device from the uploaded RangeTables, stream-ordered on s).
+int32_t ensure_chroma(TableSet& t, int groups, hipStream_t s) {
+  if (t.chroma_built) return 0;
+  if (!t.d_chroma) HIP_TRY(hipMalloc(&t.d_chroma, sizeof(ChromaTables) * t.groups_cap));
+  for (int g = 0; g < groups; ++g) HIP_TRY(build_chroma_tables(t.d_tables + g, t.d_chroma + g, s));
+  t.chroma_built = true;
+  return 0;
+}
+
+std::atomic<int> g_hot_kernel{TRIK_HSV_HOT_AUTO};
+thread_local int g_last_hot = 0;
 
 int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
                  const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, TrikHsvTargetSums* sums,
@@ -334,13 +354,25 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
     a.sums = sums;
     a.masks = masks;
     a.mask_shift = g * kRangesPerLaunch;
-    // the stripe kernel is the hot path; the generic kernel takes misaligned
-    // inputs and rows wider than 8192 pixels
-    const int e = launch_stripe(a, masks != nullptr, s);
-    if (e == hipErrorNotSupported)
-      HIP_TRY(launch_reduce(a, masks != nullptr, s));
-    else
-      HIP_TRY(e);
+    // the chroma-run kernel for large batches, the stripe kernel otherwise;
+    // the generic kernel takes misaligned inputs and rows wider than 8192 pixels
+    const int choice = g_hot_kernel.load();
+    const bool big = (int64_t)b->n_frames * b->width * b->height >= (int64_t)TRIK_HSV_CHROMA_MIN_PIXELS;
+    int e = hipErrorNotSupported;
+    if ((choice == TRIK_HSV_HOT_CHROMA || (choice == TRIK_HSV_HOT_AUTO && big)) && chroma_geometry_ok(a)) {
+      HIP_TRY(ensure_chroma(h->sums_tables, (n + kRangesPerLaunch - 1) / kRangesPerLaunch, s));
+      e = launch_chroma(a, h->sums_tables.d_chroma + g, masks != nullptr, s);
+      if (e == hipSuccess) g_last_hot = TRIK_HSV_HOT_CHROMA;
+    }
+    if (e == hipErrorNotSupported && choice != TRIK_HSV_HOT_GENERIC) {
+      e = launch_stripe(a, masks != nullptr, s);
+      if (e == hipSuccess) g_last_hot = TRIK_HSV_HOT_STRIPE;
+    }
+    if (e == hipErrorNotSupported) {
+      e = launch_reduce(a, masks != nullptr, s);
+      if (e == hipSuccess) g_last_hot = TRIK_HSV_HOT_GENERIC;
+    }
+    HIP_TRY(e);
   }
   if (!h->tables_busy) HIP_TRY(hipEventCreateWithFlags(&h->tables_busy, hipEventDisableTiming));
   HIP_TRY(hipEventRecord(h->tables_busy, s));
@@ -839,6 +871,13 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
 // ---------------------------------------------------------------------------
 // Layer 2: batched device API
 // ---------------------------------------------------------------------------
+extern "C" int32_t trik_hsv_set_hot_kernel(int32_t kind) {
+  if (kind < TRIK_HSV_HOT_AUTO || kind > TRIK_HSV_HOT_GENERIC) return -1;
+  return g_hot_kernel.exchange(kind);
+}
+
+extern "C" int32_t trik_hsv_last_hot_kernel(void) { return g_last_hot; }
+
 extern "C" const char* trik_hsv_version(void) { return "trik-hsv-mi355x 0.1.0 (gfx950)"; }
 
 extern "C" const char* trik_hsv_last_error(void) { return g_last_error.c_str(); }

@@ -1,0 +1,590 @@
+// trik_hsv_chroma.hip -- the chroma-run hot kernel for gfx950.
+//
+// Same result as the stripe kernel (the reference's WSEQ:251-284 convert +
+// WSEQ:316-354 threshold/centroid for up to 4 ranges, bit-exact), by a
+// different route that trades per-pixel arithmetic for one table lookup per
+// YUYV word:
+//
+//  * Every pixel's detection mask depends only on its (Y, U, V), and the two
+//    pixels of a YUYV word share (U, V).  For a fixed chroma c = (U, V) the
+//    mask as a function of Y ("the chroma's profile") is, for almost every c,
+//        Y <= b2 ? (Y < b1 ? M1 : M2) : 0
+//    because all three channels rise together with Y (74/64 per step) and
+//    saturate, so V rises, S falls and H stays put between saturation events.
+//    The builder (chroma_summary_kernel + chroma_block_kernel, once per range
+//    set) evaluates all 2^24 (Y,U,V) with the exact per-pixel arithmetic and
+//    stores per chroma the run descriptor b1 | b2 << 8 (16 bits; 128 KB for
+//    all chromas: it lives in LDS) and per 16-chroma block the mask pair
+//    M1 | M2 << 4.  Chromas whose profile has another shape, or whose masks
+//    differ from their block's, get the exception code kChromaExc.
+//  * The hot loop per YUYV word: one v_perm for c, three LDS reads (run
+//    descriptor, block masks, the byte-spread mask pair), two compares and two
+//    selects per pixel.  Accumulation is the stripe kernel's (byte-packed
+//    per-lane counters, lanes own chunk columns and walk rows).
+//  * Exception words are compacted into a per-wave LDS queue (ballot +
+//    mbcnt); every 64 queued words one "drain" round computes their two
+//    pixels exactly (the stripe kernel's per-pixel arithmetic, with small LDS
+//    tables: LUT43, LUT255 and the per-range H, S and V masks) and
+//    accumulates them with explicit (x, y) weights.  (Looking them up in a
+//    global 2^24-entry table instead was bound by the L1's one-line-per-clock
+//    gather rate: 0.3 ms per C3 batch.)
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "trik_hsv_internal.h"
+#include "trik_hsv_pixel.h"
+#include "trik_hsv_stripe_px.h"
+
+namespace trik_hsv {
+
+namespace {
+
+constexpr int kMaxBlock = 1024;
+constexpr int kMaxSteps = 63;
+constexpr int kQFlush = 7;
+constexpr int kQueueCap = 128;  // entries per wave: < 64 waiting + <= 64 added by one word slot
+
+// LDS image of the chroma kernel (dynamic LDS from address 0).  The block
+// masks and the mask-pair table sit below 64 KiB so their reads take an
+// immediate DS offset; the run descriptors follow.
+constexpr uint32_t kLdsBlocks = 0;                    // u16 [4096]  LDS address of the block's mask pair
+constexpr uint32_t kLdsPairs = 8192;                  // u32 [256][2] byte-spread (M1, M2) of M1 | M2 << 4
+constexpr uint32_t kLdsLut43 = 10240;                 // u16 [256]   s_mult43_div (WSEQ:389-407)
+constexpr uint32_t kLdsLut255 = kLdsLut43 + 512;      // u16 [256]   s_mult255_div
+constexpr uint32_t kLdsHue = kLdsLut255 + 512;        // u8  [256]   hue test per H (bit t = range t)
+constexpr uint32_t kLdsSat = kLdsHue + 256;           // u8  [256]   saturation test per S
+constexpr uint32_t kLdsVal = kLdsSat + 256;           // u8  [256]   value test per V
+constexpr uint32_t kLdsRuns = 12288;                  // u16 [65536] b1 | b2 << 8 per chroma
+constexpr uint32_t kLdsQueues = kLdsRuns + 131072;    // per wave: kQueueCap x {word, pos}
+static_assert(kLdsVal + 256 <= kLdsRuns, "LDS layout");
+constexpr uint32_t kLdsBytes = kLdsQueues + 16 * kQueueCap * 8;
+static_assert(kLdsBytes <= 160 * 1024, "chroma kernel LDS image");
+
+typedef __attribute__((address_space(3))) uint8_t* lds8_t;
+typedef __attribute__((address_space(3))) uint16_t* lds16_t;
+typedef __attribute__((address_space(3))) uint32_t* lds32_t;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x2* lds64_t;
+typedef __attribute__((address_space(3))) u32x4* lds128_t;
+__device__ __forceinline__ uint32_t ld8(uint32_t a) { return *(lds8_t)(uintptr_t)a; }
+__device__ __forceinline__ uint32_t ld16(uint32_t a) { return *(lds16_t)(uintptr_t)a; }
+__device__ __forceinline__ u32x2 ld64(uint32_t a) { return *(lds64_t)(uintptr_t)a; }
+__device__ __forceinline__ void st64(uint32_t a, uint32_t x, uint32_t y) {
+  u32x2 v;
+  v.x = x;
+  v.y = y;
+  *(lds64_t)(uintptr_t)a = v;
+}
+
+// 4-bit mask (range t -> bit t) -> byte-spread (range t -> bit 8t)
+__device__ __forceinline__ uint32_t spread4(uint32_t m) { return (m * 0x00204081u) & 0x01010101u; }
+
+// chroma index U | V << 8 of a YUYV word (b0=Y0, b1=U, b2=Y1, b3=V)
+__device__ __forceinline__ uint32_t chroma_of(uint32_t w) { return __builtin_amdgcn_perm(w, w, 0x0C0C0301u); }
+
+// ---------------------------------------------------------------------------
+// Builder
+// ---------------------------------------------------------------------------
+// One thread per chroma (block = V, thread = U): the exact T-bit mask for
+// every Y (the trik_hsv_pixel.h arithmetic, held to the oracle on all 2^24
+// triples by the exhaustive tests) -- the chroma's profile -- summarised as
+// its runs with the trailing zero run removed:
+//   bits 0-1 number of runs (3 = more than two), 4-7 v1, 8-11 v2,
+//   12-20 length of run 1, 21-29 length of runs 1+2.
+__global__ __launch_bounds__(256) void chroma_summary_kernel(const RangeTables* t, ChromaTables* ct) {
+  const int U = threadIdx.x, V = blockIdx.x;
+  const uint32_t c = (uint32_t)U | ((uint32_t)V << 8);
+  int nruns = 0;            // runs so far, including the current one
+  uint32_t vals[3] = {0, 0, 0};
+  int ends[3] = {0, 0, 0};  // exclusive end of each run
+  uint32_t cur = 0xFFu;
+  int last_nz_run = -1, last_nz_end = 0;
+  for (int y4 = 0; y4 < 256; y4 += 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int Y = y4 + j;
+      const uint32_t m = detect_pixel(Y, U, V, *t);
+      if (m != cur) {
+        if (nruns < 3) vals[nruns] = m;
+        ++nruns;
+        cur = m;
+      }
+      if (nruns <= 3) ends[nruns - 1] = Y + 1;
+      if (m) { last_nz_run = nruns - 1; last_nz_end = Y + 1; }
+    }
+  }
+  // runs up to and including the last nonzero one
+  const int n = last_nz_run + 1;  // 0: all zero
+  uint32_t s;
+  if (n == 0) s = 0;
+  else if (n > 2) s = 3;
+  else {
+    const int a = ends[0];
+    const int ab = n == 2 ? last_nz_end : a;
+    s = (uint32_t)n | (vals[0] << 4) | ((n == 2 ? vals[1] : 0u) << 8) | ((uint32_t)a << 12) |
+        ((uint32_t)ab << 21);
+  }
+  ct->summary[c] = s;
+}
+
+// The run descriptor of one chroma under block masks (M1, M2), or kChromaExc.
+// Semantics (chroma_kernel): e(Y) = Y <= b2 ? (Y < b1 ? M1 : M2) : 0.
+__device__ __forceinline__ uint32_t chroma_desc(uint32_t s, uint32_t M1, uint32_t M2) {
+  const uint32_t n = s & 3u;
+  if (n == 0) {  // all zero
+    if (M1 == 0) return 255u | (254u << 8);
+    if (M2 == 0) return 0u | (255u << 8);
+    return kChromaExc;
+  }
+  if (n == 3) return kChromaExc;
+  const uint32_t v1 = (s >> 4) & 15u, v2 = (s >> 8) & 15u;
+  const uint32_t a = (s >> 12) & 511u, ab = (s >> 21) & 511u;
+  if (n == 1) {
+    if (v1 == M2) return 0u | ((a - 1u) << 8);
+    if (v1 == M1 && a <= 255u) return a | ((a - 1u) << 8);
+    return kChromaExc;
+  }
+  if (v1 == M1 && v2 == M2) return a | ((ab - 1u) << 8);
+  return kChromaExc;
+}
+
+// One thread per 16-chroma block (U >> 4, V): the mask pair that represents
+// the most of its chromas (ties: the smallest M1 | M2 << 4), then the run
+// descriptors under it.
+__global__ __launch_bounds__(256) void chroma_block_kernel(ChromaTables* ct) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;  // (V << 4) | (U >> 4)
+  if (b >= 4096) return;
+  const uint32_t c0 = ((uint32_t)(b >> 4) << 8) | ((uint32_t)(b & 15) << 4);
+  uint32_t s[16];
+  uint32_t present = 1u;  // mask values appearing (value 0 always a candidate)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    s[i] = ct->summary[c0 + i];
+    if ((s[i] & 3u) == 1u || (s[i] & 3u) == 2u) {
+      present |= 1u << ((s[i] >> 4) & 15u);
+      if ((s[i] & 3u) == 2u) present |= 1u << ((s[i] >> 8) & 15u);
+    }
+  }
+  int best = -1;
+  uint32_t best_k = 0;
+  for (uint32_t k = 0; k < 256; ++k) {
+    const uint32_t M1 = k & 15u, M2 = k >> 4;
+    if (!((present >> M1) & 1u) || !((present >> M2) & 1u)) continue;
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) cnt += chroma_desc(s[i], M1, M2) != kChromaExc;
+    if (cnt > best) { best = cnt; best_k = k; }
+  }
+  ct->blocks[b] = (uint8_t)best_k;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) ct->runs[c0 + i] = (uint16_t)chroma_desc(s[i], best_k & 15u, best_k >> 4);
+}
+
+// ---------------------------------------------------------------------------
+// Hot kernel
+// ---------------------------------------------------------------------------
+struct ChromaGeom {
+  int32_t cpr, k, steps, tiles_per_frame;
+  int64_t n_tiles;
+  int32_t flush_rounds;  // drain rounds between unpacks of the 16-bit exception sums
+};
+
+template <int N>
+__device__ __forceinline__ void wave_sums(uint32_t (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x111, 0xF, 0xF, true);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x112, 0xF, 0xF, true);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x114, 0xF, 0xF, true);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x118, 0xF, 0xF, true);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x142, 0xA, 0xF, false);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x143, 0xC, 0xF, false);
+}
+
+template <int LAYOUT>
+__device__ __forceinline__ void load_chunk(const uint8_t* p, int64_t plane, uint32_t w[4]) {
+  if (LAYOUT == TRIK_HSV_LAYOUT_YUYV) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+  } else {
+    const uint2 vy = *reinterpret_cast<const uint2*>(p);
+    const uint2 vc = *reinterpret_cast<const uint2*>(p + plane);
+    // OSEQ:369-373: U = odd chroma byte, V = even chroma byte
+    w[0] = __builtin_amdgcn_perm(vc.x, vy.x, 0x04010500u);
+    w[1] = __builtin_amdgcn_perm(vc.x, vy.x, 0x06030702u);
+    w[2] = __builtin_amdgcn_perm(vc.y, vy.y, 0x04010500u);
+    w[3] = __builtin_amdgcn_perm(vc.y, vy.y, 0x06030702u);
+  }
+}
+
+__device__ __forceinline__ uint32_t pack_bits(uint32_t e) { return ((e * 0x01020408u) >> 24) & 0xFu; }
+
+// The exact mask (bit t = range t) of pixel PIX of YUYV word w: the stripe
+// kernel's arithmetic (trik_hsv_stripe_px.h: WSEQ:181-249 via v_dot4, the
+// 16-bit wrap in v_bfe) with LUT43/LUT255 and the H, S, V tests from LDS.
+template <int PIX>
+__device__ __forceinline__ uint32_t exact_mask(uint32_t w) {
+  constexpr uint32_t kY = PIX == 0 ? 74u : (74u << 16);
+  const uint32_t wc = w ^ 0xFF00FF00u;
+  const int r = stripe_px::clamp8_shift6(__builtin_amdgcn_udot4(w, kY | (102u << 24), (uint32_t)-14248, false));
+  const int g = stripe_px::clamp8_shift6(
+      __builtin_amdgcn_udot4(wc, kY | (25u << 8) | (52u << 24), (uint32_t)-10939, false));
+  const int b = stripe_px::clamp8_shift6(__builtin_amdgcn_udot4(w, kY | (129u << 8), (uint32_t)-17672, false));
+  const int mx = max(r, max(g, b)), mn = min(r, min(g, b));
+  const uint32_t d = (uint32_t)(mx - mn);
+  const int m = (int)ld16(kLdsLut43 + 2u * d);
+  const uint32_t S = (ld16(kLdsLut255 + 2u * (uint32_t)mx) * d) >> 8;
+  int h;
+  if (mx == g) h = 21845 + m * (b - r);
+  else if (mx == b) h = 43690 + m * (r - g);
+  else h = m * (g - b);
+  const uint32_t H = ((uint32_t)h >> 8) & 0xFFu;
+  return ld8(kLdsHue + H) & ld8(kLdsSat + S) & ld8(kLdsVal + (uint32_t)mx);
+}
+
+// Per-lane sums of the exception pixels a lane drained: EN byte-packed counts
+// (range t in byte t), SX/SY 16-bit fields (ranges 0,2 | 1,3) of x and of the
+// row relative to the tile's first row; unpacked into 32-bit per-range sums
+// every flush_rounds rounds and at the tile end.
+struct ExcSums {
+  uint32_t EN = 0, SX02 = 0, SX13 = 0, SY02 = 0, SY13 = 0;
+  int rounds = 0;
+};
+
+template <int LAYOUT, int NR, bool MASKS>
+__global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaGeom g, const ChromaTables* ct) {
+  const int t = threadIdx.x;
+  {  // stage block masks, the mask-pair table and the run descriptors
+#ifdef TRIK_AB_PAIR_ARITH
+    for (int i = t; i < 4096; i += blockDim.x) *(lds8_t)(uintptr_t)(kLdsBlocks + i) = ct->blocks[i];
+#else
+    for (int i = t; i < 4096; i += blockDim.x)
+      *(lds16_t)(uintptr_t)(kLdsBlocks + 2 * i) = (uint16_t)(kLdsPairs + 8u * ct->blocks[i]);
+#endif
+    for (int i = t; i < 256; i += blockDim.x) st64(kLdsPairs + 8 * i, spread4(i & 15u), spread4(i >> 4));
+    for (int i = t; i < 131072 / 16; i += blockDim.x)
+      *(lds128_t)(uintptr_t)(kLdsRuns + 16 * i) = reinterpret_cast<const u32x4*>(ct->runs)[i];
+    for (int i = t; i < 256; i += blockDim.x) {
+      *(lds16_t)(uintptr_t)(kLdsLut43 + 2 * i) = a.tables->lut43[i];
+      *(lds16_t)(uintptr_t)(kLdsLut255 + 2 * i) = a.tables->lut255[i];
+      *(lds8_t)(uintptr_t)(kLdsHue + i) = a.tables->hue[i];
+      *(lds8_t)(uintptr_t)(kLdsSat + i) = a.tables->smask[i];
+      *(lds8_t)(uintptr_t)(kLdsVal + i) = a.tables->vmask[i];
+    }
+  }
+  __syncthreads();
+
+  const int lane = t & 63;
+  const uint32_t qbase = kLdsQueues + (uint32_t)(t >> 6) * (kQueueCap * 8);
+  const uint32_t qbase_s = __builtin_amdgcn_readfirstlane(qbase);  // wave-uniform (SGPR)
+  const bool active = t < g.k * g.cpr;
+  const int col = active ? t % g.cpr : 0;
+  const int ro = active ? t / g.cpr : 0;
+  const int64_t plane = (int64_t)a.height * a.line_length;
+  const int64_t rowstep = (int64_t)g.k * a.line_length;
+  const int col_bytes = LAYOUT == TRIK_HSV_LAYOUT_YUYV ? col * 16 : col * 8;
+  const uint32_t x0 = (uint32_t)col * 8;
+  const uint32_t voff = (uint32_t)ro * (uint32_t)a.line_length + (uint32_t)col_bytes;
+
+  const int64_t t_begin = g.n_tiles * blockIdx.x / gridDim.x;
+  const int64_t t_end = g.n_tiles * (blockIdx.x + 1) / gridDim.x;
+  for (int64_t tile = t_begin; tile < t_end; ++tile) {
+    const int f = (int)(tile / g.tiles_per_frame);
+    const int r0 = (int)(tile - (int64_t)f * g.tiles_per_frame) * g.k * g.steps;
+    const int y0 = r0 + ro;
+    const int steps = min(g.steps, (a.height - r0 + g.k - 1) / g.k);
+    const uint8_t* p = a.frames + (int64_t)f * a.frame_stride + (int64_t)y0 * a.line_length + col_bytes;
+
+    uint32_t P0 = 0, P1 = 0, P2 = 0, P3 = 0, O = 0, Q = 0, CumS = 0, CumA = 0, CumB = 0;
+    uint32_t Qa = 0, Qb = 0, Ba = 0, Bb = 0;
+    int nb = 0;
+    // exception queue (wave-uniform count) and this lane's exception sums
+    int qn = 0;
+    ExcSums ex;
+    uint32_t xacc[3 * NR];
+#pragma unroll
+    for (int v = 0; v < 3 * NR; ++v) xacc[v] = 0;
+
+    auto unpack_exc = [&]() {
+#pragma unroll
+      for (int rr = 0; rr < NR; ++rr) {
+        const uint32_t sx = (rr & 1) ? ex.SX13 : ex.SX02, sy = (rr & 1) ? ex.SY13 : ex.SY02;
+        const int sh = (rr >> 1) * 16;
+        const uint32_t n = (ex.EN >> (8 * rr)) & 0xFFu;
+        xacc[3 * rr + 0] += n;
+        xacc[3 * rr + 1] += (sx >> sh) & 0xFFFFu;
+        xacc[3 * rr + 2] += ((sy >> sh) & 0xFFFFu) + (uint32_t)r0 * n;
+      }
+      ex.EN = ex.SX02 = ex.SX13 = ex.SY02 = ex.SY13 = 0;
+      ex.rounds = 0;
+    };
+    // One drain round: lanes 0..take-1 resolve queue entries 0..take-1 (two
+    // pixels each) exactly; the rest of the queue moves to the front.
+    auto drain = [&](int take) {
+      if (lane < take) {
+        const u32x2 ent = ld64(qbase + 8u * (uint32_t)lane);
+        const uint32_t w = ent.x, x = ent.y & 0xFFFFu, yr = ent.y >> 16;
+        const uint32_t m0 = exact_mask<0>(w), m1 = exact_mask<1>(w);
+        const uint32_t e0 = spread4(m0), e1 = spread4(m1);
+        if (MASKS) {
+          uint8_t* mp = a.masks + ((int64_t)f * a.height + r0 + yr) * a.width + x;
+          mp[0] = a.mask_shift ? (uint8_t)(mp[0] | (m0 << a.mask_shift)) : (uint8_t)m0;
+          mp[1] = a.mask_shift ? (uint8_t)(mp[1] | (m1 << a.mask_shift)) : (uint8_t)m1;
+        }
+        ex.EN += e0 + e1;
+        const uint32_t a0 = e0 & 0x00FF00FFu, a1 = e1 & 0x00FF00FFu;
+        const uint32_t b0 = (e0 >> 8) & 0x00FF00FFu, b1 = (e1 >> 8) & 0x00FF00FFu;
+        ex.SX02 += (a0 + a1) * x + a1;
+        ex.SX13 += (b0 + b1) * x + b1;
+        ex.SY02 += (a0 + a1) * yr;
+        ex.SY13 += (b0 + b1) * yr;
+      }
+      if (++ex.rounds == g.flush_rounds) unpack_exc();
+      const int rest = qn - take;
+      if (rest > 0) {
+        u32x2 mv = {0u, 0u};
+        if (lane < rest) mv = ld64(qbase + 8u * (uint32_t)(take + lane));
+        __builtin_amdgcn_wave_barrier();
+        if (lane < rest) st64(qbase + 8u * (uint32_t)lane, mv.x, mv.y);
+      }
+      qn = rest;
+    };
+
+    const uint8_t* pf = active ? p : a.frames + (int64_t)f * a.frame_stride;
+    const int vsteps = active ? min(steps, (a.height - y0 + g.k - 1) / g.k) : 0;
+    const bool full = (r0 + steps * g.k <= a.height) && (g.k * g.cpr) % 64 == 0;
+    const uint8_t* tbase = a.frames + (int64_t)f * a.frame_stride + (int64_t)r0 * a.line_length;
+    auto run = [&](auto full_c) {
+      constexpr bool FULL = decltype(full_c)::value;
+      // One step: the chunk's 4 words.  All LDS lookups are issued before
+      // any queue write (the queue shares LDS, so the compiler keeps the
+      // order), then the selects, then the exception words are queued.
+      auto step = [&](const uint32_t (&cw)[4], int s) {
+        const bool valid = FULL || s < vsteps;
+        uint32_t c[4], d[4], ba[4], e[8];
+        u32x2 mm[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) c[i] = chroma_of(cw[i]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          d[i] = ld16(kLdsRuns + 2u * c[i]);
+#ifdef TRIK_AB_PAIR_ARITH
+          ba[i] = *(lds8_t)(uintptr_t)(kLdsBlocks + (c[i] >> 4));
+#else
+          ba[i] = ld16(kLdsBlocks + ((c[i] >> 3) & ~1u));
+#endif
+        }
+#ifdef TRIK_AB_PAIR_ARITH
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t xk = ba[i] * 0x00204081u;
+          mm[i].x = xk & 0x01010101u;
+          mm[i].y = (xk >> 4) & 0x01010101u;
+        }
+#else
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mm[i] = ld64(ba[i]);
+#endif
+        bool exc[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          exc[i] = valid && d[i] == kChromaExc;
+          const uint32_t b1 = d[i] & 0xFFu, b2 = d[i] >> 8, w = cw[i];
+          const uint32_t Y0 = w & 0xFFu, Y1 = (w >> 16) & 0xFFu;
+          e[2 * i] = (valid && !exc[i] && Y0 <= b2) ? (Y0 < b1 ? mm[i].x : mm[i].y) : 0u;
+          e[2 * i + 1] = (valid && !exc[i] && Y1 <= b2) ? (Y1 < b1 ? mm[i].x : mm[i].y) : 0u;
+          if (MASKS && valid && !exc[i]) {
+            const int y = y0 + s * g.k;
+            uint8_t* mp = a.masks + ((int64_t)f * a.height + y) * a.width + x0 + 2 * i;
+            const uint8_t m0 = (uint8_t)(pack_bits(e[2 * i]) << a.mask_shift);
+            const uint8_t m1 = (uint8_t)(pack_bits(e[2 * i + 1]) << a.mask_shift);
+            mp[0] = a.mask_shift ? (uint8_t)(mp[0] | m0) : m0;
+            mp[1] = a.mask_shift ? (uint8_t)(mp[1] | m1) : m1;
+          }
+        }
+        const uint32_t pos_s = x0 | ((uint32_t)(ro + s * g.k) << 16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#ifdef TRIK_AB_NO_ENQUEUE
+          continue;
+#endif
+          const uint64_t bal = __builtin_amdgcn_ballot_w64(exc[i]);
+          if (bal) {
+            const uint32_t idx =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            if (exc[i]) {
+              const uint32_t qa = qbase_s + 8u * (uint32_t)qn + 8u * idx;
+              *(lds32_t)(uintptr_t)qa = cw[i];
+              *(lds32_t)(uintptr_t)(qa + 4u) = pos_s + 2u * (uint32_t)i;
+            }
+            qn += __builtin_popcountll(bal);
+#ifdef TRIK_AB_NO_DRAIN
+            if (qn >= 64) qn = 0;
+#else
+            if (qn >= 64) drain(64);
+#endif
+          }
+        }
+        P0 = P0 + e[0] + e[1];
+        P1 = P1 + e[2] + e[3];
+        P2 = P2 + e[4] + e[5];
+        P3 = P3 + e[6] + e[7];
+        O = O + e[1] + e[3];
+        O = O + e[5] + e[7];
+        Q = Q + P0 + P1;
+        Q = Q + P2 + P3;
+        ++nb;
+        if (nb == kQFlush || s + 1 == steps) {
+          const uint32_t T = Q - (uint32_t)nb * CumS;
+          Qa += T & 0x00FF00FFu;
+          Qb += (T >> 8) & 0x00FF00FFu;
+          Ba += (uint32_t)nb * CumA;
+          Bb += (uint32_t)nb * CumB;
+          CumS = P0 + P1 + P2 + P3;
+          CumA = (P0 & 0x00FF00FFu) + (P1 & 0x00FF00FFu) + (P2 & 0x00FF00FFu) + (P3 & 0x00FF00FFu);
+          CumB = ((P0 >> 8) & 0x00FF00FFu) + ((P1 >> 8) & 0x00FF00FFu) + ((P2 >> 8) & 0x00FF00FFu) +
+                 ((P3 >> 8) & 0x00FF00FFu);
+          Q = 0;
+          nb = 0;
+        }
+      };
+      const uint8_t* rb = tbase;
+      auto row_ptr = [&](int s) -> const uint8_t* {
+        if (FULL) return rb + voff;
+        return s < vsteps ? pf + (int64_t)s * rowstep : pf;
+      };
+      uint32_t wa[4], wb[4];
+      load_chunk<LAYOUT>(row_ptr(0), plane, wa);
+      for (int s = 0; s < steps; s += 2) {
+        if (FULL && s + 1 < steps) rb += rowstep;
+        load_chunk<LAYOUT>(row_ptr(s + 1), plane, wb);
+        step(wa, s);
+        if (s + 1 >= steps) break;
+        if (FULL && s + 2 < steps) rb += rowstep;
+        load_chunk<LAYOUT>(row_ptr(s + 2), plane, wa);
+        step(wb, s + 1);
+      }
+    };
+    if (full) run(std::true_type{});
+    else run(std::false_type{});
+    if (qn > 0) drain(qn);
+    unpack_exc();
+    Qa += Ba;
+    Qb += Bb;
+
+    uint32_t acc[3 * NR];
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) {
+      const int sh = 8 * rr;
+      const uint32_t c = ((rr & 1) ? (CumB >> ((rr >> 1) * 16)) : (CumA >> ((rr >> 1) * 16))) & 0xFFFFu;
+      const uint32_t wx = 2u * ((P1 >> sh) & 0xFFu) + 4u * ((P2 >> sh) & 0xFFu) +
+                          6u * ((P3 >> sh) & 0xFFu) + ((O >> sh) & 0xFFu);
+      const uint32_t qq = ((rr & 1) ? (Qb >> ((rr >> 1) * 16)) : (Qa >> ((rr >> 1) * 16))) & 0xFFFFu;
+      acc[3 * rr + 0] = c + xacc[3 * rr + 0];
+      acc[3 * rr + 1] = x0 * c + wx + xacc[3 * rr + 1];
+      acc[3 * rr + 2] = (uint32_t)y0 * c + (uint32_t)g.k * ((uint32_t)steps * c - qq) + xacc[3 * rr + 2];
+    }
+    wave_sums<3 * NR>(acc);
+    if (lane == 63) {
+      TrikHsvTargetSums* dst = a.sums + (int64_t)f * a.sums_ranges + a.range_offset;
+#pragma unroll
+      for (int v = 0; v < 3 * NR; ++v)
+        if (acc[v])
+          atomicAdd(reinterpret_cast<unsigned long long*>(&dst[v / 3].points) + (v % 3),
+                    (unsigned long long)acc[v]);
+    }
+  }
+}
+
+int cu_count() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+    return 256;
+  return n;
+}
+
+template <int LAYOUT, int NR, bool MASKS>
+int launch_t(const KernelArgs& a, const ChromaGeom& g, const ChromaTables* ct, hipStream_t s) {
+  auto kern = chroma_kernel<LAYOUT, NR, MASKS>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  static int cus = 0;
+  if (!cus) cus = cu_count();
+  const int block = ((g.k * g.cpr + 63) / 64) * 64;
+  const int64_t grid = g.n_tiles < cus ? g.n_tiles : cus;  // one workgroup per CU (LDS image)
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(block), kLdsBytes, s, a, g, ct);
+  return hipGetLastError();
+}
+
+template <int LAYOUT, bool MASKS>
+int launch_nr(const KernelArgs& a, const ChromaGeom& g, const ChromaTables* ct, hipStream_t s) {
+  switch (a.n_ranges) {
+    case 1: return launch_t<LAYOUT, 1, MASKS>(a, g, ct, s);
+    case 2: return launch_t<LAYOUT, 2, MASKS>(a, g, ct, s);
+    case 3: return launch_t<LAYOUT, 3, MASKS>(a, g, ct, s);
+    case 4: return launch_t<LAYOUT, 4, MASKS>(a, g, ct, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+int build_chroma_tables(const RangeTables* t, ChromaTables* ct, hipStream_t s) {
+  hipLaunchKernelGGL(chroma_summary_kernel, dim3(256), dim3(256), 0, s, t, ct);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(chroma_block_kernel, dim3(4096 / 256), dim3(256), 0, s, ct);
+  return hipGetLastError();
+}
+
+bool chroma_geometry_ok(const KernelArgs& a) {
+  const int cpr = a.width >> 3;
+  if (cpr <= 0 || cpr > kMaxBlock || a.height <= 0 || (a.width & 7)) return false;
+  const int64_t need = a.layout == TRIK_HSV_LAYOUT_YUYV ? 16 : 8;
+  if ((reinterpret_cast<uintptr_t>(a.frames) % need) || (a.frame_stride % need) || (a.line_length % need))
+    return false;
+  const int k = kMaxBlock / cpr;
+  const int steps_total = (a.height + k - 1) / k;
+  const int tiles = (steps_total + kMaxSteps - 1) / kMaxSteps;
+  const int steps = (steps_total + tiles - 1) / tiles;
+  // 16-bit exception sums must take at least one round (2 pixels per lane)
+  return 2LL * (a.width > steps * k ? a.width : steps * k) <= 65535;
+}
+
+int launch_chroma(const KernelArgs& a, const ChromaTables* ct, bool write_masks, hipStream_t s) {
+  if (!chroma_geometry_ok(a)) return hipErrorNotSupported;
+  ChromaGeom g;
+  g.cpr = a.width >> 3;
+  g.k = kMaxBlock / g.cpr;
+  const int steps_total = (a.height + g.k - 1) / g.k;
+  g.tiles_per_frame = (steps_total + kMaxSteps - 1) / kMaxSteps;
+  g.steps = (steps_total + g.tiles_per_frame - 1) / g.tiles_per_frame;
+  g.n_tiles = (int64_t)g.tiles_per_frame * a.n_frames;
+  // per round a lane adds <= 2 pixels: byte counts <= 2r, x sums <= 2r*W, row sums <= 2r*rows
+  {
+    const int span = a.width > g.steps * g.k ? a.width : g.steps * g.k;
+    int r = 65535 / (2 * span);
+    if (r > 127) r = 127;
+    g.flush_rounds = r < 1 ? 1 : r;
+  }
+  if (g.n_tiles == 0) return hipSuccess;
+  if (a.layout == TRIK_HSV_LAYOUT_YUYV)
+    return write_masks ? launch_nr<TRIK_HSV_LAYOUT_YUYV, true>(a, g, ct, s)
+                       : launch_nr<TRIK_HSV_LAYOUT_YUYV, false>(a, g, ct, s);
+  return write_masks ? launch_nr<TRIK_HSV_LAYOUT_OV7670, true>(a, g, ct, s)
+                     : launch_nr<TRIK_HSV_LAYOUT_OV7670, false>(a, g, ct, s);
+}
+
+}  // namespace trik_hsv

@@ -20,13 +20,17 @@ constexpr int kRangesPerLaunch = 4;
 //                       S = (LUT255[mx] * (mx - mn)) >> 8 (WSEQ:223-224), V = mx.
 //   hue[H]            : bit t = range t's hue test passes (incl. wrap, WSEQ:433-445).
 //   lut43[d], lut255[m] : s_mult43_div, s_mult255_div (WSEQ:389-407).
+//   smask[S], vmask[V] : bit t = range t's saturation / value test passes
+//                       (the two factors of sv, for the chroma kernel's exact path).
 struct alignas(16) RangeTables {
   uint8_t sv[256 * 256];
   uint8_t hue[256];
   uint16_t lut43[256];
   uint16_t lut255[256];
+  uint8_t smask[256];
+  uint8_t vmask[256];
 };
-static_assert(sizeof(RangeTables) == 65536 + 256 + 512 + 512, "table layout");
+static_assert(sizeof(RangeTables) == 65536 + 256 + 512 + 512 + 512, "table layout");
 
 // Packed form of one InArgs range (WSEQ:425-445).
 struct PackedRange {
@@ -53,6 +57,20 @@ struct alignas(16) StripeTables {
 };
 static_assert(sizeof(StripeTables) == 66560 + 256 * 4 * (kHueCopies + kM43Copies), "table layout");
 static_assert(2 * sizeof(StripeTables) <= 160 * 1024, "two workgroups per CU");
+
+// Tables of the chroma-run kernel (trik_hsv_chroma.hip), one set per group of
+// <= 4 ranges, built on the device from RangeTables:
+//   runs[c]     : run descriptor b1 | b2 << 8 of chroma c = U | V << 8: the
+//                 pixel mask is Y <= b2 ? (Y < b1 ? M1 : M2) : 0, or
+//                 kChromaExc when the chroma's profile has another shape
+//   blocks[b]   : M1 | M2 << 4 (4-bit masks) of block b = c >> 4
+//   summary[c]  : builder scratch (run summary of the chroma's profile)
+constexpr uint32_t kChromaExc = 0x00FFu;  // b1 = 255, b2 = 0: never a built descriptor
+struct alignas(16) ChromaTables {
+  uint16_t runs[65536];
+  uint8_t blocks[4096];
+  uint32_t summary[65536];
+};
 
 PackedRange pack_range(const TRIK_VIDTRANSCODE_CV_InArgsAlg& r);
 void compile_tables(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTables* out);
@@ -123,6 +141,12 @@ int launch_reduce(const KernelArgs& a, bool write_masks, hipStream_t s);
 // The optimised hot kernel (trik_hsv_stripe.hip); returns hipErrorNotSupported
 // when the geometry needs the generic kernel (misaligned input, width > 8192).
 int launch_stripe(const KernelArgs& a, bool write_masks, hipStream_t s);
+// The chroma-run hot kernel (trik_hsv_chroma.hip): tables built once per
+// range set; launch returns hipErrorNotSupported when the geometry needs
+// another kernel.
+int build_chroma_tables(const RangeTables* t, ChromaTables* ct, hipStream_t s);
+bool chroma_geometry_ok(const KernelArgs& a);
+int launch_chroma(const KernelArgs& a, const ChromaTables* ct, bool write_masks, hipStream_t s);
 int launch_targets(const TrikHsvFrameBatch& b, int n_ranges, const TrikHsvTargetSums* sums,
                    TrikHsvTarget* targets, hipStream_t s);
 int launch_synth(const TrikHsvFrameBatch& b, uint8_t* frames, int first_frame, int kind,

@@ -57,6 +57,10 @@ void compile_tables(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTa
     const uint32_t fv = (p.from >> 16) & 0xFF, tv = (p.to >> 16) & 0xFF;
     for (uint32_t h = 0; h < 256; ++h)
       if ((outside(h, fh, th) ? 1u : 0u) == (p.expect & 1u)) out->hue[h] |= bit;
+    for (uint32_t x = 0; x < 256; ++x) {
+      if (!outside(x, fs, ts)) out->smask[x] |= bit;
+      if (!outside(x, fv, tv)) out->vmask[x] |= bit;
+    }
     for (uint32_t mx = 0; mx < 256; ++mx) {
       if (outside(mx, fv, tv)) continue;
       for (uint32_t mn = 0; mn <= mx; ++mn) {

@@ -259,6 +259,24 @@ def batch_auto_range(frames, width, height, line_length, layout, *, n_frames=Non
     return out
 
 
+HOT_AUTO, HOT_STRIPE, HOT_CHROMA, HOT_GENERIC = 0, 1, 2, 3
+
+
+def set_hot_kernel(kind: int) -> int:
+    """Select the hot kernel of the batched sums (process-wide): HOT_AUTO (the
+    chroma-run kernel for large batches), HOT_STRIPE, HOT_CHROMA or
+    HOT_GENERIC.  Returns the previous setting.  Results are identical."""
+    prev = _lib.trik_hsv_set_hot_kernel(int(kind))
+    if prev < 0:
+        raise ValueError(f"unknown hot kernel {kind}")
+    return prev
+
+
+def last_hot_kernel() -> int:
+    """The kernel the last batched-sums launch on this thread ran."""
+    return _lib.trik_hsv_last_hot_kernel()
+
+
 def batch_targets(sums, width, height, *, stream=None):
     """Epilogue only: sums int64 [N,T,3] -> targets int8 [N,T,4]."""
     import torch

@@ -198,6 +198,8 @@ PROTOTYPES = {
     "trik_hsv_blob_preview": ([C.c_void_p, C.POINTER(FrameBatch), C.c_void_p, C.c_void_p, i32, i32, i32,
                                C.c_void_p, C.c_int64, C.c_void_p], i32),
     "trik_hsv_synth": ([C.POINTER(FrameBatch), i32, i32, u64, C.c_void_p], i32),
+    "trik_hsv_set_hot_kernel": ([i32], i32),
+    "trik_hsv_last_hot_kernel": ([], i32),
 }
 
 _lib = None
