@@ -41,14 +41,20 @@ namespace trik_hsv {
 namespace {
 
 constexpr int kMaxBlock = 1024;
-constexpr int kMaxSteps = 63;
+#ifndef TRIK_CHROMA_CW
+#define TRIK_CHROMA_CW 8
+#endif
+constexpr int kChunkWords = TRIK_CHROMA_CW;  // YUYV words per lane and row (8: 32 bytes, 16 pixels)
+static_assert(kChunkWords == 4 || kChunkWords == 8, "chunk width");
+// steps per tile: byte counters P_i <= 2 * steps, O <= kChunkWords * steps
+constexpr int kMaxSteps = kChunkWords == 8 ? 31 : 63;
 constexpr int kQFlush = 7;
 constexpr int kQueueCap = 128;  // entries per wave: < 64 waiting + <= 64 added by one word slot
 
 // LDS image of the chroma kernel (dynamic LDS from address 0).  The block
 // masks and the mask-pair table sit below 64 KiB so their reads take an
 // immediate DS offset; the run descriptors follow.
-constexpr uint32_t kLdsBlocks = 0;                    // u16 [4096]  LDS address of the block's mask pair
+constexpr uint32_t kLdsBlocks = 0;                    // u8  [4096]  M1 | M2 << 4 of the 16-chroma block
 constexpr uint32_t kLdsPairs = 8192;                  // u32 [256][2] byte-spread (M1, M2) of M1 | M2 << 4
 constexpr uint32_t kLdsLut43 = 10240;                 // u16 [256]   s_mult43_div (WSEQ:389-407)
 constexpr uint32_t kLdsLut255 = kLdsLut43 + 512;      // u16 [256]   s_mult255_div
@@ -58,7 +64,8 @@ constexpr uint32_t kLdsVal = kLdsSat + 256;           // u8  [256]   value test 
 constexpr uint32_t kLdsRuns = 12288;                  // u16 [65536] b1 | b2 << 8 per chroma
 constexpr uint32_t kLdsQueues = kLdsRuns + 131072;    // per wave: kQueueCap x {word, pos}
 static_assert(kLdsVal + 256 <= kLdsRuns, "LDS layout");
-constexpr uint32_t kLdsBytes = kLdsQueues + 16 * kQueueCap * 8;
+constexpr uint32_t kLdsZeroPair = kLdsQueues + 16 * kQueueCap * 8;  // 8 zero bytes above 64 KiB
+constexpr uint32_t kLdsBytes = kLdsZeroPair + 8;
 static_assert(kLdsBytes <= 160 * 1024, "chroma kernel LDS image");
 
 typedef __attribute__((address_space(3))) uint8_t* lds8_t;
@@ -76,6 +83,27 @@ __device__ __forceinline__ void st64(uint32_t a, uint32_t x, uint32_t y) {
   v.x = x;
   v.y = y;
   *(lds64_t)(uintptr_t)a = v;
+}
+
+// The two pixels of YUYV word w under run descriptor d = b1 | b2 << 8 and
+// mask pair (m1, m2): e = Y <= b2 ? (Y < b1 ? m1 : m2) : 0.  Byte operands
+// straight from w and d by SDWA selects; the four compares precede the
+// selects, which gives the VALU-writes-SGPR -> v_cndmask distance gfx950
+// needs without nops.
+__device__ __forceinline__ void select2(uint32_t w, uint16_t d, uint32_t m1, uint32_t m2, uint32_t& e0,
+                                        uint32_t& e1) {
+  uint64_t lt0, lt1, le0, le1;
+  asm volatile(
+      "v_cmp_gt_u32_sdwa %[lt0], %[d], %[w] src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"
+      "v_cmp_gt_u32_sdwa %[lt1], %[d], %[w] src0_sel:BYTE_0 src1_sel:BYTE_2\n\t"
+      "v_cmp_ge_u32_sdwa %[le0], %[d], %[w] src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"
+      "v_cmp_ge_u32_sdwa %[le1], %[d], %[w] src0_sel:BYTE_1 src1_sel:BYTE_2\n\t"
+      "v_cndmask_b32_e64 %[e0], %[m2], %[m1], %[lt0]\n\t"
+      "v_cndmask_b32_e64 %[e1], %[m2], %[m1], %[lt1]\n\t"
+      "v_cndmask_b32_e64 %[e0], 0, %[e0], %[le0]\n\t"
+      "v_cndmask_b32_e64 %[e1], 0, %[e1], %[le1]"
+      : [lt0] "=&s"(lt0), [lt1] "=&s"(lt1), [le0] "=&s"(le0), [le1] "=&s"(le1), [e0] "=&v"(e0), [e1] "=&v"(e1)
+      : [w] "v"(w), [d] "v"(d), [m1] "v"(m1), [m2] "v"(m2));
 }
 
 // 4-bit mask (range t -> bit t) -> byte-spread (range t -> bit 8t)
@@ -207,19 +235,35 @@ __device__ __forceinline__ void wave_sums(uint32_t (&v)[N]) {
   for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x143, 0xC, 0xF, false);
 }
 
-template <int LAYOUT>
-__device__ __forceinline__ void load_chunk(const uint8_t* p, int64_t plane, uint32_t w[4]) {
+// One chunk = CW YUYV words (2*CW pixels) of a row: CW*4 bytes packed, or
+// 2*CW luma + 2*CW chroma bytes of the ov7670 planes.
+template <int LAYOUT, int CW>
+__device__ __forceinline__ void load_chunk(const uint8_t* p, int64_t plane, uint32_t (&w)[CW]) {
   if (LAYOUT == TRIK_HSV_LAYOUT_YUYV) {
-    const uint4 v = *reinterpret_cast<const uint4*>(p);
-    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+#pragma unroll
+    for (int j = 0; j < CW / 4; ++j) {
+      const uint4 v = reinterpret_cast<const uint4*>(p)[j];
+      w[4 * j + 0] = v.x; w[4 * j + 1] = v.y; w[4 * j + 2] = v.z; w[4 * j + 3] = v.w;
+    }
   } else {
-    const uint2 vy = *reinterpret_cast<const uint2*>(p);
-    const uint2 vc = *reinterpret_cast<const uint2*>(p + plane);
+    uint32_t yy[CW / 2], cc[CW / 2];
+    if (CW == 8) {
+      const uint4 vy = *reinterpret_cast<const uint4*>(p);
+      const uint4 vc = *reinterpret_cast<const uint4*>(p + plane);
+      yy[0] = vy.x; yy[1] = vy.y; yy[CW / 2 - 2] = vy.z; yy[CW / 2 - 1] = vy.w;
+      cc[0] = vc.x; cc[1] = vc.y; cc[CW / 2 - 2] = vc.z; cc[CW / 2 - 1] = vc.w;
+    } else {
+      const uint2 vy = *reinterpret_cast<const uint2*>(p);
+      const uint2 vc = *reinterpret_cast<const uint2*>(p + plane);
+      yy[0] = vy.x; yy[CW / 2 - 1] = vy.y;
+      cc[0] = vc.x; cc[CW / 2 - 1] = vc.y;
+    }
     // OSEQ:369-373: U = odd chroma byte, V = even chroma byte
-    w[0] = __builtin_amdgcn_perm(vc.x, vy.x, 0x04010500u);
-    w[1] = __builtin_amdgcn_perm(vc.x, vy.x, 0x06030702u);
-    w[2] = __builtin_amdgcn_perm(vc.y, vy.y, 0x04010500u);
-    w[3] = __builtin_amdgcn_perm(vc.y, vy.y, 0x06030702u);
+#pragma unroll
+    for (int j = 0; j < CW / 2; ++j) {
+      w[2 * j] = __builtin_amdgcn_perm(cc[j], yy[j], 0x04010500u);
+      w[2 * j + 1] = __builtin_amdgcn_perm(cc[j], yy[j], 0x06030702u);
+    }
   }
 }
 
@@ -257,17 +301,14 @@ struct ExcSums {
   int rounds = 0;
 };
 
-template <int LAYOUT, int NR, bool MASKS>
+template <int LAYOUT, int NR, bool MASKS, int CW>
 __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaGeom g, const ChromaTables* ct) {
   const int t = threadIdx.x;
   {  // stage block masks, the mask-pair table and the run descriptors
-#ifdef TRIK_AB_PAIR_ARITH
-    for (int i = t; i < 4096; i += blockDim.x) *(lds8_t)(uintptr_t)(kLdsBlocks + i) = ct->blocks[i];
-#else
-    for (int i = t; i < 4096; i += blockDim.x)
-      *(lds16_t)(uintptr_t)(kLdsBlocks + 2 * i) = (uint16_t)(kLdsPairs + 8u * ct->blocks[i]);
-#endif
+    for (int i = t; i < 4096 / 16; i += blockDim.x)
+      *(lds128_t)(uintptr_t)(kLdsBlocks + 16 * i) = reinterpret_cast<const u32x4*>(ct->blocks)[i];
     for (int i = t; i < 256; i += blockDim.x) st64(kLdsPairs + 8 * i, spread4(i & 15u), spread4(i >> 4));
+    if (t == 0) st64(kLdsZeroPair, 0u, 0u);
     for (int i = t; i < 131072 / 16; i += blockDim.x)
       *(lds128_t)(uintptr_t)(kLdsRuns + 16 * i) = reinterpret_cast<const u32x4*>(ct->runs)[i];
     for (int i = t; i < 256; i += blockDim.x) {
@@ -288,8 +329,9 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
   const int ro = active ? t / g.cpr : 0;
   const int64_t plane = (int64_t)a.height * a.line_length;
   const int64_t rowstep = (int64_t)g.k * a.line_length;
-  const int col_bytes = LAYOUT == TRIK_HSV_LAYOUT_YUYV ? col * 16 : col * 8;
-  const uint32_t x0 = (uint32_t)col * 8;
+  constexpr int kQBlock = CW == 8 ? 5 : kQFlush;  // Q block: CW * n * (n + 1) <= 255
+  const int col_bytes = LAYOUT == TRIK_HSV_LAYOUT_YUYV ? col * 4 * CW : col * 2 * CW;
+  const uint32_t x0 = (uint32_t)col * 2 * CW;
   const uint32_t voff = (uint32_t)ro * (uint32_t)a.line_length + (uint32_t)col_bytes;
 
   const int64_t t_begin = g.n_tiles * blockIdx.x / gridDim.x;
@@ -301,7 +343,9 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     const int steps = min(g.steps, (a.height - r0 + g.k - 1) / g.k);
     const uint8_t* p = a.frames + (int64_t)f * a.frame_stride + (int64_t)y0 * a.line_length + col_bytes;
 
-    uint32_t P0 = 0, P1 = 0, P2 = 0, P3 = 0, O = 0, Q = 0, CumS = 0, CumA = 0, CumB = 0;
+    uint32_t P[CW], O = 0, Q = 0, CumS = 0, CumA = 0, CumB = 0;
+#pragma unroll
+    for (int i = 0; i < CW; ++i) P[i] = 0;
     uint32_t Qa = 0, Qb = 0, Ba = 0, Bb = 0;
     int nb = 0;
     // exception queue (wave-uniform count) and this lane's exception sums
@@ -365,40 +409,32 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
       // One step: the chunk's 4 words.  All LDS lookups are issued before
       // any queue write (the queue shares LDS, so the compiler keeps the
       // order), then the selects, then the exception words are queued.
-      auto step = [&](const uint32_t (&cw)[4], int s) {
+      auto step = [&](const uint32_t (&cw)[CW], int s) {
         const bool valid = FULL || s < vsteps;
-        uint32_t c[4], d[4], ba[4], e[8];
-        u32x2 mm[4];
+        uint32_t c[CW], ba[CW], e[2 * CW];
+        uint16_t d[CW];
+        u32x2 mm[CW];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) c[i] = chroma_of(cw[i]);
+        for (int i = 0; i < CW; ++i) c[i] = chroma_of(cw[i]);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          d[i] = ld16(kLdsRuns + 2u * c[i]);
-#ifdef TRIK_AB_PAIR_ARITH
-          ba[i] = *(lds8_t)(uintptr_t)(kLdsBlocks + (c[i] >> 4));
-#else
-          ba[i] = ld16(kLdsBlocks + ((c[i] >> 3) & ~1u));
-#endif
+        for (int i = 0; i < CW; ++i) {
+          d[i] = *(lds16_t)(uintptr_t)(kLdsRuns + 2u * c[i]);
+          ba[i] = kLdsPairs + 8u * *(lds8_t)(uintptr_t)(kLdsBlocks + (c[i] >> 4));
         }
-#ifdef TRIK_AB_PAIR_ARITH
+        // Exception words (and rows past the frame) read an all-zero mask
+        // pair, so the selects below need no per-pixel gating.  (The zero
+        // pair sits above 64 KiB so the select stays 32-bit.)
+        bool exc[CW];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t xk = ba[i] * 0x00204081u;
-          mm[i].x = xk & 0x01010101u;
-          mm[i].y = (xk >> 4) & 0x01010101u;
+        for (int i = 0; i < CW; ++i) {
+          exc[i] = valid & (d[i] == (uint16_t)kChromaExc);
+          ba[i] = (exc[i] | !valid) ? kLdsZeroPair : ba[i];
         }
-#else
 #pragma unroll
-        for (int i = 0; i < 4; ++i) mm[i] = ld64(ba[i]);
-#endif
-        bool exc[4];
+        for (int i = 0; i < CW; ++i) mm[i] = ld64(ba[i]);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          exc[i] = valid && d[i] == kChromaExc;
-          const uint32_t b1 = d[i] & 0xFFu, b2 = d[i] >> 8, w = cw[i];
-          const uint32_t Y0 = w & 0xFFu, Y1 = (w >> 16) & 0xFFu;
-          e[2 * i] = (valid && !exc[i] && Y0 <= b2) ? (Y0 < b1 ? mm[i].x : mm[i].y) : 0u;
-          e[2 * i + 1] = (valid && !exc[i] && Y1 <= b2) ? (Y1 < b1 ? mm[i].x : mm[i].y) : 0u;
+        for (int i = 0; i < CW; ++i) {
+          select2(cw[i], d[i], mm[i].x, mm[i].y, e[2 * i], e[2 * i + 1]);
           if (MASKS && valid && !exc[i]) {
             const int y = y0 + s * g.k;
             uint8_t* mp = a.masks + ((int64_t)f * a.height + y) * a.width + x0 + 2 * i;
@@ -410,8 +446,8 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         }
         const uint32_t pos_s = x0 | ((uint32_t)(ro + s * g.k) << 16);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-#ifdef TRIK_AB_NO_ENQUEUE
+        for (int i = 0; i < CW; ++i) {
+#ifdef TRIK_AB_NO_ENQUEUE  // timing attribution only (drops the exception words)
           continue;
 #endif
           const uint64_t bal = __builtin_amdgcn_ballot_w64(exc[i]);
@@ -424,32 +460,35 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
               *(lds32_t)(uintptr_t)(qa + 4u) = pos_s + 2u * (uint32_t)i;
             }
             qn += __builtin_popcountll(bal);
-#ifdef TRIK_AB_NO_DRAIN
+#ifdef TRIK_AB_NO_DRAIN  // timing attribution only (drops the exception words)
             if (qn >= 64) qn = 0;
 #else
             if (qn >= 64) drain(64);
 #endif
           }
         }
-        P0 = P0 + e[0] + e[1];
-        P1 = P1 + e[2] + e[3];
-        P2 = P2 + e[4] + e[5];
-        P3 = P3 + e[6] + e[7];
-        O = O + e[1] + e[3];
-        O = O + e[5] + e[7];
-        Q = Q + P0 + P1;
-        Q = Q + P2 + P3;
+#pragma unroll
+        for (int i = 0; i < CW; ++i) P[i] = P[i] + e[2 * i] + e[2 * i + 1];
+#pragma unroll
+        for (int i = 0; i < CW; i += 2) O = O + e[2 * i + 1] + e[2 * i + 3];
+#pragma unroll
+        for (int i = 0; i < CW; i += 2) Q = Q + P[i] + P[i + 1];
         ++nb;
-        if (nb == kQFlush || s + 1 == steps) {
+        if (nb == kQBlock || s + 1 == steps) {
           const uint32_t T = Q - (uint32_t)nb * CumS;
           Qa += T & 0x00FF00FFu;
           Qb += (T >> 8) & 0x00FF00FFu;
           Ba += (uint32_t)nb * CumA;
           Bb += (uint32_t)nb * CumB;
-          CumS = P0 + P1 + P2 + P3;
-          CumA = (P0 & 0x00FF00FFu) + (P1 & 0x00FF00FFu) + (P2 & 0x00FF00FFu) + (P3 & 0x00FF00FFu);
-          CumB = ((P0 >> 8) & 0x00FF00FFu) + ((P1 >> 8) & 0x00FF00FFu) + ((P2 >> 8) & 0x00FF00FFu) +
-                 ((P3 >> 8) & 0x00FF00FFu);
+          CumS = 0;
+          CumA = 0;
+          CumB = 0;
+#pragma unroll
+          for (int i = 0; i < CW; ++i) {
+            CumS += P[i];
+            CumA += P[i] & 0x00FF00FFu;
+            CumB += (P[i] >> 8) & 0x00FF00FFu;
+          }
           Q = 0;
           nb = 0;
         }
@@ -459,15 +498,15 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         if (FULL) return rb + voff;
         return s < vsteps ? pf + (int64_t)s * rowstep : pf;
       };
-      uint32_t wa[4], wb[4];
-      load_chunk<LAYOUT>(row_ptr(0), plane, wa);
+      uint32_t wa[CW], wb[CW];
+      load_chunk<LAYOUT, CW>(row_ptr(0), plane, wa);
       for (int s = 0; s < steps; s += 2) {
         if (FULL && s + 1 < steps) rb += rowstep;
-        load_chunk<LAYOUT>(row_ptr(s + 1), plane, wb);
+        load_chunk<LAYOUT, CW>(row_ptr(s + 1), plane, wb);
         step(wa, s);
         if (s + 1 >= steps) break;
         if (FULL && s + 2 < steps) rb += rowstep;
-        load_chunk<LAYOUT>(row_ptr(s + 2), plane, wa);
+        load_chunk<LAYOUT, CW>(row_ptr(s + 2), plane, wa);
         step(wb, s + 1);
       }
     };
@@ -483,8 +522,9 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     for (int rr = 0; rr < NR; ++rr) {
       const int sh = 8 * rr;
       const uint32_t c = ((rr & 1) ? (CumB >> ((rr >> 1) * 16)) : (CumA >> ((rr >> 1) * 16))) & 0xFFFFu;
-      const uint32_t wx = 2u * ((P1 >> sh) & 0xFFu) + 4u * ((P2 >> sh) & 0xFFu) +
-                          6u * ((P3 >> sh) & 0xFFu) + ((O >> sh) & 0xFFu);
+      uint32_t wx = (O >> sh) & 0xFFu;
+#pragma unroll
+      for (int i = 1; i < CW; ++i) wx += 2u * (uint32_t)i * ((P[i] >> sh) & 0xFFu);
       const uint32_t qq = ((rr & 1) ? (Qb >> ((rr >> 1) * 16)) : (Qa >> ((rr >> 1) * 16))) & 0xFFFFu;
       acc[3 * rr + 0] = c + xacc[3 * rr + 0];
       acc[3 * rr + 1] = x0 * c + wx + xacc[3 * rr + 1];
@@ -512,7 +552,7 @@ int cu_count() {
 
 template <int LAYOUT, int NR, bool MASKS>
 int launch_t(const KernelArgs& a, const ChromaGeom& g, const ChromaTables* ct, hipStream_t s) {
-  auto kern = chroma_kernel<LAYOUT, NR, MASKS>;
+  auto kern = chroma_kernel<LAYOUT, NR, MASKS, kChunkWords>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -549,36 +589,43 @@ int build_chroma_tables(const RangeTables* t, ChromaTables* ct, hipStream_t s) {
   return hipGetLastError();
 }
 
-bool chroma_geometry_ok(const KernelArgs& a) {
-  const int cpr = a.width >> 3;
-  if (cpr <= 0 || cpr > kMaxBlock || a.height <= 0 || (a.width & 7)) return false;
-  const int64_t need = a.layout == TRIK_HSV_LAYOUT_YUYV ? 16 : 8;
+// Column chunks of 2*kChunkWords pixels; k rows per step, as many as fit a
+// 1024-lane workgroup, rounded down to whole waves when that keeps >= 7/8 of
+// the lanes (the kernel's uniform fast path needs whole waves).
+bool chroma_geometry(const KernelArgs& a, ChromaGeom& g) {
+  const int px = 2 * kChunkWords;
+  if (a.width <= 0 || a.width % px || a.height <= 0) return false;
+  const int cpr = a.width / px;
+  if (cpr > kMaxBlock) return false;
+  const int64_t need = 16;  // vector loads
   if ((reinterpret_cast<uintptr_t>(a.frames) % need) || (a.frame_stride % need) || (a.line_length % need))
     return false;
-  const int k = kMaxBlock / cpr;
+  int k = kMaxBlock / cpr;
+  for (int kk = k; kk * 8 >= k * 7; --kk)
+    if ((kk * cpr) % 64 == 0) { k = kk; break; }
+  g.cpr = cpr;
+  g.k = k;
   const int steps_total = (a.height + k - 1) / k;
-  const int tiles = (steps_total + kMaxSteps - 1) / kMaxSteps;
-  const int steps = (steps_total + tiles - 1) / tiles;
-  // 16-bit exception sums must take at least one round (2 pixels per lane)
-  return 2LL * (a.width > steps * k ? a.width : steps * k) <= 65535;
-}
-
-int launch_chroma(const KernelArgs& a, const ChromaTables* ct, bool write_masks, hipStream_t s) {
-  if (!chroma_geometry_ok(a)) return hipErrorNotSupported;
-  ChromaGeom g;
-  g.cpr = a.width >> 3;
-  g.k = kMaxBlock / g.cpr;
-  const int steps_total = (a.height + g.k - 1) / g.k;
   g.tiles_per_frame = (steps_total + kMaxSteps - 1) / kMaxSteps;
   g.steps = (steps_total + g.tiles_per_frame - 1) / g.tiles_per_frame;
   g.n_tiles = (int64_t)g.tiles_per_frame * a.n_frames;
-  // per round a lane adds <= 2 pixels: byte counts <= 2r, x sums <= 2r*W, row sums <= 2r*rows
-  {
-    const int span = a.width > g.steps * g.k ? a.width : g.steps * g.k;
-    int r = 65535 / (2 * span);
-    if (r > 127) r = 127;
-    g.flush_rounds = r < 1 ? 1 : r;
-  }
+  // per drain round a lane adds <= 2 pixels: byte counts <= 2r, x sums <= 2r*W,
+  // row sums <= 2r*rows; the 16-bit sums must take at least one round
+  const int span = a.width > g.steps * k ? a.width : g.steps * k;
+  if (2LL * span > 65535) return false;
+  int r = 65535 / (2 * span);
+  g.flush_rounds = r > 127 ? 127 : r;
+  return true;
+}
+
+bool chroma_geometry_ok(const KernelArgs& a) {
+  ChromaGeom g;
+  return chroma_geometry(a, g);
+}
+
+int launch_chroma(const KernelArgs& a, const ChromaTables* ct, bool write_masks, hipStream_t s) {
+  ChromaGeom g;
+  if (!chroma_geometry(a, g)) return hipErrorNotSupported;
   if (g.n_tiles == 0) return hipSuccess;
   if (a.layout == TRIK_HSV_LAYOUT_YUYV)
     return write_masks ? launch_nr<TRIK_HSV_LAYOUT_YUYV, true>(a, g, ct, s)
