@@ -41,6 +41,9 @@ namespace trik_hsv {
 namespace {
 
 constexpr int kMaxBlock = 1024;
+#ifndef TRIK_CHROMA_PF
+#define TRIK_CHROMA_PF 1  // rows prefetched ahead of the one being processed
+#endif
 #ifndef TRIK_CHROMA_CW
 #define TRIK_CHROMA_CW 8
 #endif
@@ -418,23 +421,40 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         for (int i = 0; i < CW; ++i) c[i] = chroma_of(cw[i]);
 #pragma unroll
         for (int i = 0; i < CW; ++i) {
+#ifdef TRIK_AB_NO_LDS  // timing attribution only
+          d[i] = (uint16_t)(c[i] * 0x9E37u);
+          ba[i] = kLdsPairs + 8u * (c[i] >> 12);
+#else
           d[i] = *(lds16_t)(uintptr_t)(kLdsRuns + 2u * c[i]);
           ba[i] = kLdsPairs + 8u * *(lds8_t)(uintptr_t)(kLdsBlocks + (c[i] >> 4));
+#endif
         }
         // Exception words (and rows past the frame) read an all-zero mask
         // pair, so the selects below need no per-pixel gating.  (The zero
         // pair sits above 64 KiB so the select stays 32-bit.)
         bool exc[CW];
+        uint64_t bal[CW];  // exc as wave masks (SGPR pairs), for the queue
 #pragma unroll
         for (int i = 0; i < CW; ++i) {
           exc[i] = valid & (d[i] == (uint16_t)kChromaExc);
+          bal[i] = __builtin_amdgcn_ballot_w64(exc[i]);
           ba[i] = (exc[i] | !valid) ? kLdsZeroPair : ba[i];
         }
+#ifdef TRIK_AB_NO_LDS
+#pragma unroll
+        for (int i = 0; i < CW; ++i) { mm[i].x = ba[i] & 0x01010101u; mm[i].y = (ba[i] >> 1) & 0x01010101u; }
+#else
 #pragma unroll
         for (int i = 0; i < CW; ++i) mm[i] = ld64(ba[i]);
+#endif
 #pragma unroll
         for (int i = 0; i < CW; ++i) {
+#ifdef TRIK_AB_STREAM  // timing attribution only: no detection at all
+          e[2 * i] = cw[i] & 0x01010101u;
+          e[2 * i + 1] = (cw[i] >> 1) & 0x01010101u;
+#else
           select2(cw[i], d[i], mm[i].x, mm[i].y, e[2 * i], e[2 * i + 1]);
+#endif
           if (MASKS && valid && !exc[i]) {
             const int y = y0 + s * g.k;
             uint8_t* mp = a.masks + ((int64_t)f * a.height + y) * a.width + x0 + 2 * i;
@@ -450,16 +470,15 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
 #ifdef TRIK_AB_NO_ENQUEUE  // timing attribution only (drops the exception words)
           continue;
 #endif
-          const uint64_t bal = __builtin_amdgcn_ballot_w64(exc[i]);
-          if (bal) {
-            const uint32_t idx =
-                __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-            if (exc[i]) {
-              const uint32_t qa = qbase_s + 8u * (uint32_t)qn + 8u * idx;
+          if (bal[i]) {
+            const uint32_t idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[i] >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bal[i], 0u));
+            if (__builtin_amdgcn_inverse_ballot_w64(bal[i])) {
+              const uint32_t qa = __builtin_amdgcn_readfirstlane(qbase_s + 8u * (uint32_t)qn) + 8u * idx;
               *(lds32_t)(uintptr_t)qa = cw[i];
               *(lds32_t)(uintptr_t)(qa + 4u) = pos_s + 2u * (uint32_t)i;
             }
-            qn += __builtin_popcountll(bal);
+            qn += __builtin_popcountll(bal[i]);
 #ifdef TRIK_AB_NO_DRAIN  // timing attribution only (drops the exception words)
             if (qn >= 64) qn = 0;
 #else
@@ -493,6 +512,27 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
           nb = 0;
         }
       };
+#if TRIK_CHROMA_PF == 2
+      // rows prefetched two steps ahead (three buffers, unrolled by 3); loads
+      // past the tile's last step re-read its last row
+      auto row_ptr = [&](int s) -> const uint8_t* {
+        if (FULL) return tbase + (int64_t)(s < steps ? s : steps - 1) * rowstep + voff;
+        return s < vsteps ? pf + (int64_t)s * rowstep : pf;
+      };
+      uint32_t wa[CW], wb[CW], wc[CW];
+      load_chunk<LAYOUT, CW>(row_ptr(0), plane, wa);
+      load_chunk<LAYOUT, CW>(row_ptr(1), plane, wb);
+      for (int s = 0; s < steps; s += 3) {
+        load_chunk<LAYOUT, CW>(row_ptr(s + 2), plane, wc);
+        step(wa, s);
+        if (s + 1 >= steps) break;
+        load_chunk<LAYOUT, CW>(row_ptr(s + 3), plane, wa);
+        step(wb, s + 1);
+        if (s + 2 >= steps) break;
+        load_chunk<LAYOUT, CW>(row_ptr(s + 4), plane, wb);
+        step(wc, s + 2);
+      }
+#else
       const uint8_t* rb = tbase;
       auto row_ptr = [&](int s) -> const uint8_t* {
         if (FULL) return rb + voff;
@@ -509,6 +549,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         load_chunk<LAYOUT, CW>(row_ptr(s + 2), plane, wa);
         step(wb, s + 1);
       }
+#endif
     };
     if (full) run(std::true_type{});
     else run(std::false_type{});
