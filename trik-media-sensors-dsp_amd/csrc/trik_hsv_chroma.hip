@@ -287,11 +287,12 @@ __device__ __forceinline__ uint32_t exact_mask(uint32_t w) {
   const uint32_t d = (uint32_t)(mx - mn);
   const int m = (int)ld16(kLdsLut43 + 2u * d);
   const uint32_t S = (ld16(kLdsLut255 + 2u * (uint32_t)mx) * d) >> 8;
-  int h;
-  if (mx == g) h = 21845 + m * (b - r);
-  else if (mx == b) h = 43690 + m * (r - g);
-  else h = m * (g - b);
-  const uint32_t H = ((uint32_t)h >> 8) & 0xFFu;
+  // hue case select as in stripe_px::phase1 (G > B > R on ties), branch-free
+  const bool eqG = mx == g, eqB = mx == b;
+  const int dR = g - b, dG = b - r, dB = r - g;
+  const int diff = eqG ? dG : (eqB ? dB : dR);
+  const int base = eqG ? 21845 : (eqB ? 43690 : 0);
+  const uint32_t H = ((uint32_t)(base + m * diff) >> 8) & 0xFFu;
   return ld8(kLdsHue + H) & ld8(kLdsSat + S) & ld8(kLdsVal + (uint32_t)mx);
 }
 
