@@ -471,7 +471,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
 #ifdef TRIK_AB_NO_ENQUEUE  // timing attribution only (drops the exception words)
           continue;
 #endif
-          if (bal[i]) {
+          {  // (a branch on bal != 0 would almost never skip: some lane has an exception in nearly every slot)
             const uint32_t idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[i] >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bal[i], 0u));
             if (__builtin_amdgcn_inverse_ballot_w64(bal[i])) {
