@@ -67,8 +67,7 @@ constexpr uint32_t kLdsVal = kLdsSat + 256;           // u8  [256]   value test 
 constexpr uint32_t kLdsRuns = 12288;                  // u16 [65536] b1 | b2 << 8 per chroma
 constexpr uint32_t kLdsQueues = kLdsRuns + 131072;    // per wave: kQueueCap x {word, pos}
 static_assert(kLdsVal + 256 <= kLdsRuns, "LDS layout");
-constexpr uint32_t kLdsZeroPair = kLdsQueues + 16 * kQueueCap * 8;  // 8 zero bytes above 64 KiB
-constexpr uint32_t kLdsBytes = kLdsZeroPair + 8;
+constexpr uint32_t kLdsBytes = kLdsQueues + 16 * kQueueCap * 8;
 static_assert(kLdsBytes <= 160 * 1024, "chroma kernel LDS image");
 
 typedef __attribute__((address_space(3))) uint8_t* lds8_t;
@@ -88,25 +87,35 @@ __device__ __forceinline__ void st64(uint32_t a, uint32_t x, uint32_t y) {
   *(lds64_t)(uintptr_t)a = v;
 }
 
-// The two pixels of YUYV word w under run descriptor d = b1 | b2 << 8 and
-// mask pair (m1, m2): e = Y <= b2 ? (Y < b1 ? m1 : m2) : 0.  Byte operands
-// straight from w and d by SDWA selects; the four compares precede the
-// selects, which gives the VALU-writes-SGPR -> v_cndmask distance gfx950
-// needs without nops.
-__device__ __forceinline__ void select2(uint32_t w, uint16_t d, uint32_t m1, uint32_t m2, uint32_t& e0,
-                                        uint32_t& e1) {
-  uint64_t lt0, lt1, le0, le1;
+// The fast-path masks of the two pixels of YUYV word w under run descriptor
+// d = b1 | b2 << 8 and mask pair (m1, m2): with lt = Y < b1, le = Y <= b2,
+// e = le ? (lt ? m1 : m2) : 0.  Byte operands straight from w and d by SDWA
+// compares; the selects follow all compares (the VALU-writes-SGPR ->
+// v_cndmask distance needs no nops).  q0 / q1 (wave masks, SALU) flag the
+// pixels the exact path resolves: a window pixel (lt and not le, where the
+// select gives 0) or any pixel of an exception-code word (le is cleared, so
+// the select gives 0 as well).  vm masks lanes without a valid row.
+__device__ __forceinline__ void select2(uint32_t w, uint32_t d, uint32_t m1, uint32_t m2, uint64_t vm,
+                                        uint32_t& e0, uint32_t& e1, uint64_t& q0, uint64_t& q1) {
+  uint64_t x, lt0, lt1, le0, le1;
   asm volatile(
+      "v_cmp_eq_u32_e64 %[x], %[k], %[d]\n\t"
       "v_cmp_gt_u32_sdwa %[lt0], %[d], %[w] src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"
       "v_cmp_gt_u32_sdwa %[lt1], %[d], %[w] src0_sel:BYTE_0 src1_sel:BYTE_2\n\t"
       "v_cmp_ge_u32_sdwa %[le0], %[d], %[w] src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"
-      "v_cmp_ge_u32_sdwa %[le1], %[d], %[w] src0_sel:BYTE_1 src1_sel:BYTE_2\n\t"
+      "v_cmp_ge_u32_sdwa %[le1], %[d], %[w] src0_sel:BYTE_1 src1_sel:BYTE_2"
+      : [x] "=&s"(x), [lt0] "=&s"(lt0), [lt1] "=&s"(lt1), [le0] "=&s"(le0), [le1] "=&s"(le1)
+      : [w] "v"(w), [d] "v"(d), [k] "s"(kChromaExc));
+  q0 = (x | (lt0 & ~le0)) & vm;
+  q1 = (x | (lt1 & ~le1)) & vm;
+  const uint64_t k0 = le0 & ~x & vm, k1 = le1 & ~x & vm;
+  asm volatile(
       "v_cndmask_b32_e64 %[e0], %[m2], %[m1], %[lt0]\n\t"
       "v_cndmask_b32_e64 %[e1], %[m2], %[m1], %[lt1]\n\t"
-      "v_cndmask_b32_e64 %[e0], 0, %[e0], %[le0]\n\t"
-      "v_cndmask_b32_e64 %[e1], 0, %[e1], %[le1]"
-      : [lt0] "=&s"(lt0), [lt1] "=&s"(lt1), [le0] "=&s"(le0), [le1] "=&s"(le1), [e0] "=&v"(e0), [e1] "=&v"(e1)
-      : [w] "v"(w), [d] "v"(d), [m1] "v"(m1), [m2] "v"(m2));
+      "v_cndmask_b32_e64 %[e0], 0, %[e0], %[k0]\n\t"
+      "v_cndmask_b32_e64 %[e1], 0, %[e1], %[k1]"
+      : [e0] "=&v"(e0), [e1] "=&v"(e1)
+      : [m1] "v"(m1), [m2] "v"(m2), [lt0] "s"(lt0), [lt1] "s"(lt1), [k0] "s"(k0), [k1] "s"(k1));
 }
 
 // 4-bit mask (range t -> bit t) -> byte-spread (range t -> bit 8t)
@@ -150,18 +159,23 @@ __global__ __launch_bounds__(256) void chroma_summary_kernel(const RangeTables* 
   const int n = last_nz_run + 1;  // 0: all zero
   uint32_t s;
   if (n == 0) s = 0;
-  else if (n > 2) s = 3;
   else {
+    // a: end of the first run (its value v1 = the mask at Y = 0, maybe 0);
+    // ab: end of run 2 (n == 2) or of the last nonzero run (n > 2)
     const int a = ends[0];
-    const int ab = n == 2 ? last_nz_end : a;
-    s = (uint32_t)n | (vals[0] << 4) | ((n == 2 ? vals[1] : 0u) << 8) | ((uint32_t)a << 12) |
+    const int ab = n == 1 ? a : last_nz_end;
+    s = (uint32_t)(n > 2 ? 3 : n) | (vals[0] << 4) | ((n == 2 ? vals[1] : 0u) << 8) | ((uint32_t)a << 12) |
         ((uint32_t)ab << 21);
   }
   ct->summary[c] = s;
 }
 
-// The run descriptor of one chroma under block masks (M1, M2), or kChromaExc.
-// Semantics (chroma_kernel): e(Y) = Y <= b2 ? (Y < b1 ? M1 : M2) : 0.
+// The run descriptor of one chroma under block masks (M1, M2).  With
+// lt = Y < b1 and le = Y <= b2 the hot kernel's mask is le ? (lt ? M1 : M2) : 0:
+//  * b1 <= b2 + 1 ("runs"): M1 on [0, b1), M2 on [b1, b2], 0 above b2;
+//  * b1 >  b2 + 1 ("window"): M1 on [0, b2], 0 on [b1, 255], and the pixels
+//    with b2 < Y < b1 (lt and not le: the select gives 0) are computed exactly;
+//  * kChromaExc: both pixels of the word are computed exactly (le is masked).
 __device__ __forceinline__ uint32_t chroma_desc(uint32_t s, uint32_t M1, uint32_t M2) {
   const uint32_t n = s & 3u;
   if (n == 0) {  // all zero
@@ -169,21 +183,33 @@ __device__ __forceinline__ uint32_t chroma_desc(uint32_t s, uint32_t M1, uint32_
     if (M2 == 0) return 0u | (255u << 8);
     return kChromaExc;
   }
-  if (n == 3) return kChromaExc;
   const uint32_t v1 = (s >> 4) & 15u, v2 = (s >> 8) & 15u;
   const uint32_t a = (s >> 12) & 511u, ab = (s >> 21) & 511u;
   if (n == 1) {
     if (v1 == M2) return 0u | ((a - 1u) << 8);
     if (v1 == M1 && a <= 255u) return a | ((a - 1u) << 8);
-    return kChromaExc;
   }
-  if (v1 == M1 && v2 == M2) return a | ((ab - 1u) << 8);
-  return kChromaExc;
+  if (n == 2 && v1 == M1 && v2 == M2) return a | ((ab - 1u) << 8);
+  // window: the profile must be M1 at Y = 0 and 0 at Y = 255
+  if (v1 != M1 || ab > 255u) return kChromaExc;
+  const uint32_t b2 = a - 1u, b1 = ab;
+  if (b2 == 0u && b1 == 255u) return kChromaExc;  // that window is the exception code
+  return b1 | (b2 << 8);
 }
 
-// One thread per 16-chroma block (U >> 4, V): the mask pair that represents
-// the most of its chromas (ties: the smallest M1 | M2 << 4), then the run
-// descriptors under it.
+// Expected exact-path words per 65536 words of a chroma (uniform Y): a window
+// of L values flags a word with probability 1 - (1 - L/256)^2.
+__device__ __forceinline__ uint32_t chroma_cost(uint32_t d) {
+  if (d == kChromaExc) return 65536u;
+  const uint32_t b1 = d & 255u, b2 = d >> 8;
+  if (b1 <= b2 + 1u) return 0u;
+  const uint32_t L = b1 - b2 - 1u;
+  return L * (512u - L);
+}
+
+// One thread per 16-chroma block (U >> 4, V): the mask pair with the fewest
+// expected exact-path words over its chromas (ties: the smallest
+// M1 | M2 << 4), then the run descriptors under it.
 __global__ __launch_bounds__(256) void chroma_block_kernel(ChromaTables* ct) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;  // (V << 4) | (U >> 4)
   if (b >= 4096) return;
@@ -193,20 +219,17 @@ __global__ __launch_bounds__(256) void chroma_block_kernel(ChromaTables* ct) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     s[i] = ct->summary[c0 + i];
-    if ((s[i] & 3u) == 1u || (s[i] & 3u) == 2u) {
-      present |= 1u << ((s[i] >> 4) & 15u);
-      if ((s[i] & 3u) == 2u) present |= 1u << ((s[i] >> 8) & 15u);
-    }
+    if (s[i] & 3u) present |= 1u << ((s[i] >> 4) & 15u);
+    if ((s[i] & 3u) == 2u) present |= 1u << ((s[i] >> 8) & 15u);
   }
-  int best = -1;
-  uint32_t best_k = 0;
+  uint32_t best = 0xFFFFFFFFu, best_k = 0;
   for (uint32_t k = 0; k < 256; ++k) {
     const uint32_t M1 = k & 15u, M2 = k >> 4;
     if (!((present >> M1) & 1u) || !((present >> M2) & 1u)) continue;
-    int cnt = 0;
+    uint32_t cost = 0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) cnt += chroma_desc(s[i], M1, M2) != kChromaExc;
-    if (cnt > best) { best = cnt; best_k = k; }
+    for (int i = 0; i < 16; ++i) cost += chroma_cost(chroma_desc(s[i], M1, M2));
+    if (cost < best) { best = cost; best_k = k; }
   }
   ct->blocks[b] = (uint8_t)best_k;
 #pragma unroll
@@ -312,7 +335,6 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     for (int i = t; i < 4096 / 16; i += blockDim.x)
       *(lds128_t)(uintptr_t)(kLdsBlocks + 16 * i) = reinterpret_cast<const u32x4*>(ct->blocks)[i];
     for (int i = t; i < 256; i += blockDim.x) st64(kLdsPairs + 8 * i, spread4(i & 15u), spread4(i >> 4));
-    if (t == 0) st64(kLdsZeroPair, 0u, 0u);
     for (int i = t; i < 131072 / 16; i += blockDim.x)
       *(lds128_t)(uintptr_t)(kLdsRuns + 16 * i) = reinterpret_cast<const u32x4*>(ct->runs)[i];
     for (int i = t; i < 256; i += blockDim.x) {
@@ -378,12 +400,17 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
       if (lane < take) {
         const u32x2 ent = ld64(qbase + 8u * (uint32_t)lane);
         const uint32_t w = ent.x, x = ent.y & 0xFFFFu, yr = ent.y >> 16;
-        const uint32_t m0 = exact_mask<0>(w), m1 = exact_mask<1>(w);
+        // which of the word's pixels the fast path left to this path (select2)
+        const uint32_t d = ld16(kLdsRuns + 2u * chroma_of(w));
+        const uint32_t lo = d & 0xFFu, hi = d >> 8, Y0 = w & 0xFFu, Y1 = (w >> 16) & 0xFFu;
+        const bool xw = d == kChromaExc;
+        const bool f0 = xw | ((Y0 < lo) & (Y0 > hi)), f1 = xw | ((Y1 < lo) & (Y1 > hi));
+        const uint32_t m0 = f0 ? exact_mask<0>(w) : 0u, m1 = f1 ? exact_mask<1>(w) : 0u;
         const uint32_t e0 = spread4(m0), e1 = spread4(m1);
         if (MASKS) {
           uint8_t* mp = a.masks + ((int64_t)f * a.height + r0 + yr) * a.width + x;
-          mp[0] = a.mask_shift ? (uint8_t)(mp[0] | (m0 << a.mask_shift)) : (uint8_t)m0;
-          mp[1] = a.mask_shift ? (uint8_t)(mp[1] | (m1 << a.mask_shift)) : (uint8_t)m1;
+          if (f0) mp[0] = a.mask_shift ? (uint8_t)(mp[0] | (m0 << a.mask_shift)) : (uint8_t)m0;
+          if (f1) mp[1] = a.mask_shift ? (uint8_t)(mp[1] | (m1 << a.mask_shift)) : (uint8_t)m1;
         }
         ex.EN += e0 + e1;
         const uint32_t a0 = e0 & 0x00FF00FFu, a1 = e1 & 0x00FF00FFu;
@@ -415,31 +442,22 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
       // order), then the selects, then the exception words are queued.
       auto step = [&](const uint32_t (&cw)[CW], int s) {
         const bool valid = FULL || s < vsteps;
-        uint32_t c[CW], ba[CW], e[2 * CW];
-        uint16_t d[CW];
+        // lanes with a valid row (rows past the frame re-read a valid row:
+        // their pixels are masked out of the sums and the queue)
+        const uint64_t vm = FULL ? ~0ull : __builtin_amdgcn_ballot_w64(valid);
+        uint32_t c[CW], ba[CW], d[CW], e[2 * CW];
         u32x2 mm[CW];
 #pragma unroll
         for (int i = 0; i < CW; ++i) c[i] = chroma_of(cw[i]);
 #pragma unroll
         for (int i = 0; i < CW; ++i) {
 #ifdef TRIK_AB_NO_LDS  // timing attribution only
-          d[i] = (uint16_t)(c[i] * 0x9E37u);
+          d[i] = (c[i] * 0x9E37u) & 0xFFFFu;
           ba[i] = kLdsPairs + 8u * (c[i] >> 12);
 #else
-          d[i] = *(lds16_t)(uintptr_t)(kLdsRuns + 2u * c[i]);
-          ba[i] = kLdsPairs + 8u * *(lds8_t)(uintptr_t)(kLdsBlocks + (c[i] >> 4));
+          d[i] = ld16(kLdsRuns + 2u * c[i]);
+          ba[i] = kLdsPairs + 8u * ld8(kLdsBlocks + (c[i] >> 4));
 #endif
-        }
-        // Exception words (and rows past the frame) read an all-zero mask
-        // pair, so the selects below need no per-pixel gating.  (The zero
-        // pair sits above 64 KiB so the select stays 32-bit.)
-        bool exc[CW];
-        uint64_t bal[CW];  // exc as wave masks (SGPR pairs), for the queue
-#pragma unroll
-        for (int i = 0; i < CW; ++i) {
-          exc[i] = valid & (d[i] == (uint16_t)kChromaExc);
-          bal[i] = __builtin_amdgcn_ballot_w64(exc[i]);
-          ba[i] = (exc[i] | !valid) ? kLdsZeroPair : ba[i];
         }
 #ifdef TRIK_AB_NO_LDS
 #pragma unroll
@@ -448,44 +466,45 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
 #pragma unroll
         for (int i = 0; i < CW; ++i) mm[i] = ld64(ba[i]);
 #endif
+        // per word: the selects, then the words with a pixel for the exact
+        // path (a wave mask in SGPRs) are queued
+        const uint32_t pos_s = x0 | ((uint32_t)(ro + s * g.k) << 16);
 #pragma unroll
         for (int i = 0; i < CW; ++i) {
+          uint64_t q0, q1;
 #ifdef TRIK_AB_STREAM  // timing attribution only: no detection at all
           e[2 * i] = cw[i] & 0x01010101u;
           e[2 * i + 1] = (cw[i] >> 1) & 0x01010101u;
+          q0 = q1 = 0;
 #else
-          select2(cw[i], d[i], mm[i].x, mm[i].y, e[2 * i], e[2 * i + 1]);
+          select2(cw[i], d[i], mm[i].x, mm[i].y, vm, e[2 * i], e[2 * i + 1], q0, q1);
 #endif
-          if (MASKS && valid && !exc[i]) {
+          const uint64_t bal = q0 | q1;
+          if (MASKS && valid) {  // verification mode: the exact path writes the flagged pixels
             const int y = y0 + s * g.k;
             uint8_t* mp = a.masks + ((int64_t)f * a.height + y) * a.width + x0 + 2 * i;
             const uint8_t m0 = (uint8_t)(pack_bits(e[2 * i]) << a.mask_shift);
             const uint8_t m1 = (uint8_t)(pack_bits(e[2 * i + 1]) << a.mask_shift);
-            mp[0] = a.mask_shift ? (uint8_t)(mp[0] | m0) : m0;
-            mp[1] = a.mask_shift ? (uint8_t)(mp[1] | m1) : m1;
+            if (!__builtin_amdgcn_inverse_ballot_w64(q0)) mp[0] = a.mask_shift ? (uint8_t)(mp[0] | m0) : m0;
+            if (!__builtin_amdgcn_inverse_ballot_w64(q1)) mp[1] = a.mask_shift ? (uint8_t)(mp[1] | m1) : m1;
           }
-        }
-        const uint32_t pos_s = x0 | ((uint32_t)(ro + s * g.k) << 16);
-#pragma unroll
-        for (int i = 0; i < CW; ++i) {
-#ifdef TRIK_AB_NO_ENQUEUE  // timing attribution only (drops the exception words)
-          continue;
-#endif
-          {  // (a branch on bal != 0 would almost never skip: some lane has an exception in nearly every slot)
-            const uint32_t idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[i] >> 32),
-                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bal[i], 0u));
-            if (__builtin_amdgcn_inverse_ballot_w64(bal[i])) {
-              const uint32_t qa = __builtin_amdgcn_readfirstlane(qbase_s + 8u * (uint32_t)qn) + 8u * idx;
-              *(lds32_t)(uintptr_t)qa = cw[i];
-              *(lds32_t)(uintptr_t)(qa + 4u) = pos_s + 2u * (uint32_t)i;
-            }
-            qn += __builtin_popcountll(bal[i]);
+#ifndef TRIK_AB_NO_ENQUEUE  // timing attribution only (drops the exception words)
+          // (a branch on bal != 0 would seldom skip: some lane of the wave has a
+          // flagged word in most slots)
+          const uint32_t idx =
+              __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+          if (__builtin_amdgcn_inverse_ballot_w64(bal)) {
+            const uint32_t qa = __builtin_amdgcn_readfirstlane(qbase_s + 8u * (uint32_t)qn) + 8u * idx;
+            *(lds32_t)(uintptr_t)qa = cw[i];
+            *(lds32_t)(uintptr_t)(qa + 4u) = pos_s + 2u * (uint32_t)i;
+          }
+          qn += __builtin_popcountll(bal);
 #ifdef TRIK_AB_NO_DRAIN  // timing attribution only (drops the exception words)
-            if (qn >= 64) qn = 0;
+          if (qn >= 64) qn = 0;
 #else
-            if (qn >= 64) drain(64);
+          if (qn >= 64) drain(64);
 #endif
-          }
+#endif
         }
 #pragma unroll
         for (int i = 0; i < CW; ++i) P[i] = P[i] + e[2 * i] + e[2 * i + 1];
