@@ -466,6 +466,11 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
 #pragma unroll
         for (int i = 0; i < CW; ++i) mm[i] = ld64(ba[i]);
 #endif
+        // pin the descriptors as 32-bit values here (ds_read_u16 zero-extends):
+        // otherwise the zero extension is sunk past the drain branches and
+        // costs a v_and per word
+#pragma unroll
+        for (int i = 0; i < CW; ++i) asm volatile("" : "+v"(d[i]));
         // per word: the selects, then the words with a pixel for the exact
         // path (a wave mask in SGPRs) are queued
         const uint32_t pos_s = x0 | ((uint32_t)(ro + s * g.k) << 16);
