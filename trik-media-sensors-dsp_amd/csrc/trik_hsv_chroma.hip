@@ -7,27 +7,31 @@
 //
 //  * Every pixel's detection mask depends only on its (Y, U, V), and the two
 //    pixels of a YUYV word share (U, V).  For a fixed chroma c = (U, V) the
-//    mask as a function of Y ("the chroma's profile") is, for almost every c,
+//    mask as a function of Y ("the chroma's profile") is, for most c,
 //        Y <= b2 ? (Y < b1 ? M1 : M2) : 0
 //    because all three channels rise together with Y (74/64 per step) and
 //    saturate, so V rises, S falls and H stays put between saturation events.
 //    The builder (chroma_summary_kernel + chroma_block_kernel, once per range
 //    set) evaluates all 2^24 (Y,U,V) with the exact per-pixel arithmetic and
-//    stores per chroma the run descriptor b1 | b2 << 8 (16 bits; 128 KB for
-//    all chromas: it lives in LDS) and per 16-chroma block the mask pair
-//    M1 | M2 << 4.  Chromas whose profile has another shape, or whose masks
-//    differ from their block's, get the exception code kChromaExc.
+//    stores per chroma the descriptor b1 | b2 << 8 (16 bits; 128 KB for all
+//    chromas: it lives in LDS) and per 16-chroma block the mask pair
+//    M1 | M2 << 4.  A descriptor with b1 > b2 + 1 is a "window": the same
+//    select gives M1 below it and 0 above it, and the pixels inside it
+//    (b2 < Y < b1) are flagged for the exact path -- so a chroma of another
+//    shape costs only the pixels in its window.  The exception code
+//    kChromaExc flags both pixels of the word.
 //  * The hot loop per YUYV word: one v_perm for c, three LDS reads (run
-//    descriptor, block masks, the byte-spread mask pair), two compares and two
-//    selects per pixel.  Accumulation is the stripe kernel's (byte-packed
-//    per-lane counters, lanes own chunk columns and walk rows).
-//  * Exception words are compacted into a per-wave LDS queue (ballot +
-//    mbcnt); every 64 queued words one "drain" round computes their two
-//    pixels exactly (the stripe kernel's per-pixel arithmetic, with small LDS
+//    descriptor, block masks, the byte-spread mask pair), five compares and
+//    four selects; the flags are SALU operations on the compare masks.
+//    Accumulation is the stripe kernel's (byte-packed per-lane counters,
+//    lanes own chunk columns and walk rows).
+//  * Flagged words are compacted into a per-wave LDS queue (ballot + mbcnt);
+//    every 64 queued words one "drain" round computes their flagged pixels
+//    exactly (the stripe kernel's per-pixel arithmetic, with small LDS
 //    tables: LUT43, LUT255 and the per-range H, S and V masks) and
 //    accumulates them with explicit (x, y) weights.  (Looking them up in a
-//    global 2^24-entry table instead was bound by the L1's one-line-per-clock
-//    gather rate: 0.3 ms per C3 batch.)
+//    global per-(Y, c) table instead was slower: the gather's latency is
+//    exposed in the drain.)
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -132,7 +136,8 @@ __device__ __forceinline__ uint32_t chroma_of(uint32_t w) { return __builtin_amd
 // triples by the exhaustive tests) -- the chroma's profile -- summarised as
 // its runs with the trailing zero run removed:
 //   bits 0-1 number of runs (3 = more than two), 4-7 v1, 8-11 v2,
-//   12-20 length of run 1, 21-29 length of runs 1+2.
+//   12-20 end of run 1, 21-29 end of run 2 (two runs) or of the last nonzero
+//   run (more than two).
 __global__ __launch_bounds__(256) void chroma_summary_kernel(const RangeTables* t, ChromaTables* ct) {
   const int U = threadIdx.x, V = blockIdx.x;
   const uint32_t c = (uint32_t)U | ((uint32_t)V << 8);
@@ -366,7 +371,8 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     const int f = (int)(tile / g.tiles_per_frame);
     const int r0 = (int)(tile - (int64_t)f * g.tiles_per_frame) * g.k * g.steps;
     const int y0 = r0 + ro;
-    const int steps = min(g.steps, (a.height - r0 + g.k - 1) / g.k);
+    // wave-uniform (the division runs on the VALU): keeps the step loop scalar
+    const int steps = __builtin_amdgcn_readfirstlane(min(g.steps, (a.height - r0 + g.k - 1) / g.k));
     const uint8_t* p = a.frames + (int64_t)f * a.frame_stride + (int64_t)y0 * a.line_length + col_bytes;
 
     uint32_t P[CW], O = 0, Q = 0, CumS = 0, CumA = 0, CumB = 0;

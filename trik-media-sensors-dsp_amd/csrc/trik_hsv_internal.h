@@ -60,12 +60,13 @@ static_assert(2 * sizeof(StripeTables) <= 160 * 1024, "two workgroups per CU");
 
 // Tables of the chroma-run kernel (trik_hsv_chroma.hip), one set per group of
 // <= 4 ranges, built on the device from RangeTables:
-//   runs[c]     : run descriptor b1 | b2 << 8 of chroma c = U | V << 8: the
-//                 pixel mask is Y <= b2 ? (Y < b1 ? M1 : M2) : 0, or
-//                 kChromaExc when the chroma's profile has another shape
+//   runs[c]     : descriptor b1 | b2 << 8 of chroma c = U | V << 8: the
+//                 fast path's mask is Y <= b2 ? (Y < b1 ? M1 : M2) : 0; with
+//                 b1 > b2 + 1 the pixels b2 < Y < b1 go to the exact path
+//                 (a "window"), and kChromaExc sends both pixels there
 //   blocks[b]   : M1 | M2 << 4 (4-bit masks) of block b = c >> 4
 //   summary[c]  : builder scratch (run summary of the chroma's profile)
-constexpr uint32_t kChromaExc = 0x00FFu;  // b1 = 255, b2 = 0: never a built descriptor
+constexpr uint32_t kChromaExc = 0x00FFu;  // b1 = 255, b2 = 0: the builder never makes this window
 struct alignas(16) ChromaTables {
   uint16_t runs[65536];
   uint8_t blocks[4096];
