@@ -1,6 +1,7 @@
 """CPU model of the chroma-run hot kernel's tables (trik_hsv_chroma.hip:
-chroma_summary_kernel, chroma_desc, chroma_block_kernel, select2), restated in
-numpy and checked against the oracle's exact mask of every (Y, U, V).
+chroma_summary_kernel, chroma_desc, chroma_block_kernel, chroma_palette_kernel,
+select2), restated in numpy and checked against the oracle's exact mask of
+every (Y, U, V).
 
 It pins the descriptor semantics independently of the device: for every
 chroma the fast path's select `le ? (lt ? M1 : M2) : 0` (lt = Y < b1,
@@ -92,6 +93,16 @@ def build(P):
         better = ok & (c < best)
         best[better] = c[better]
         best_k[better] = k
+    # chroma_palette_kernel: the 32 most used pairs (ties: smaller k); a block
+    # whose pair missed the palette takes the cheapest palette pair
+    hist = np.bincount(best_k, minlength=256)
+    order = sorted(range(256), key=lambda k: (-hist[k], k))
+    palette = [k for k in order[:32] if hist[k] > 0]
+    miss = ~np.isin(best_k, palette)
+    if miss.any():
+        costs = np.stack([cost(desc(S, np.full(65536, k & 15), np.full(65536, k >> 4))).reshape(4096, 16).sum(1)
+                          for k in palette], axis=1)
+        best_k = np.where(miss, np.asarray(palette)[np.argmin(costs, axis=1)], best_k)
     kk = np.repeat(best_k, 16)
     return desc(S, kk & 15, kk >> 4), best_k
 

@@ -15,7 +15,7 @@
 //    set) evaluates all 2^24 (Y,U,V) with the exact per-pixel arithmetic and
 //    stores per chroma the descriptor b1 | b2 << 8 (16 bits; 128 KB for all
 //    chromas: it lives in LDS) and per 16-chroma block the mask pair
-//    M1 | M2 << 4.  A descriptor with b1 > b2 + 1 is a "window": the same
+//    M1 | M2 << 4 (stored as its offset in a palette of <= 32 pairs).  A descriptor with b1 > b2 + 1 is a "window": the same
 //    select gives M1 below it and 0 above it, and the pixels inside it
 //    (b2 < Y < b1) are flagged for the exact path -- so a chroma of another
 //    shape costs only the pixels in its window.  The exception code
@@ -62,7 +62,7 @@ constexpr int kQueueCap = 128;  // entries per wave: < 64 waiting + <= 64 added 
 // masks and the mask-pair table sit below 64 KiB so their reads take an
 // immediate DS offset; the run descriptors follow.
 constexpr uint32_t kLdsBlocks = 0;                    // u8  [4096]  M1 | M2 << 4 of the 16-chroma block
-constexpr uint32_t kLdsPairs = 8192;                  // u32 [256][2] byte-spread (M1, M2) of M1 | M2 << 4
+constexpr uint32_t kLdsPairs = 8192;                  // u32 [kChromaPalette][2] byte-spread (M1, M2) of the palette
 constexpr uint32_t kLdsLut43 = 10240;                 // u16 [256]   s_mult43_div (WSEQ:389-407)
 constexpr uint32_t kLdsLut255 = kLdsLut43 + 512;      // u16 [256]   s_mult255_div
 constexpr uint32_t kLdsHue = kLdsLut255 + 512;        // u8  [256]   hue test per H (bit t = range t)
@@ -214,7 +214,11 @@ __device__ __forceinline__ uint32_t chroma_cost(uint32_t d) {
 
 // One thread per 16-chroma block (U >> 4, V): the mask pair with the fewest
 // expected exact-path words over its chromas (ties: the smallest
-// M1 | M2 << 4), then the run descriptors under it.
+// k = M1 | M2 << 4).  PALETTE = false: the unrestricted choice, counted in
+// pair_hist.  PALETTE = true: the choice among the palette's pairs (the
+// unrestricted one when it made the palette, which is nearly always), then
+// the block byte (the pair's palette offset) and the run descriptors under it.
+template <bool PALETTE>
 __global__ __launch_bounds__(256) void chroma_block_kernel(ChromaTables* ct) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;  // (V << 4) | (U >> 4)
   if (b >= 4096) return;
@@ -227,18 +231,50 @@ __global__ __launch_bounds__(256) void chroma_block_kernel(ChromaTables* ct) {
     if (s[i] & 3u) present |= 1u << ((s[i] >> 4) & 15u);
     if ((s[i] & 3u) == 2u) present |= 1u << ((s[i] >> 8) & 15u);
   }
-  uint32_t best = 0xFFFFFFFFu, best_k = 0;
-  for (uint32_t k = 0; k < 256; ++k) {
-    const uint32_t M1 = k & 15u, M2 = k >> 4;
-    if (!((present >> M1) & 1u) || !((present >> M2) & 1u)) continue;
+  auto block_cost = [&](uint32_t k) {
     uint32_t cost = 0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) cost += chroma_cost(chroma_desc(s[i], M1, M2));
-    if (cost < best) { best = cost; best_k = k; }
+    for (int i = 0; i < 16; ++i) cost += chroma_cost(chroma_desc(s[i], k & 15u, k >> 4));
+    return cost;
+  };
+  uint32_t best = 0xFFFFFFFFu, best_k = 0;
+  if (!PALETTE || ct->palette_of[ct->blocks[b]] == 0xFFu) {
+    for (uint32_t k = 0; k < 256; ++k) {
+      if (PALETTE ? ct->palette_of[k] == 0xFFu : (!((present >> (k & 15u)) & 1u) || !((present >> (k >> 4)) & 1u)))
+        continue;
+      const uint32_t cost = block_cost(k);
+      if (cost < best) { best = cost; best_k = k; }
+    }
+  } else {
+    best_k = ct->blocks[b];
   }
-  ct->blocks[b] = (uint8_t)best_k;
+  if (!PALETTE) {
+    ct->blocks[b] = (uint8_t)best_k;
+    atomicAdd(&ct->pair_hist[best_k], 1u);
+    return;
+  }
+  ct->blocks[b] = ct->palette_of[best_k];
 #pragma unroll
   for (int i = 0; i < 16; ++i) ct->runs[c0 + i] = (uint16_t)chroma_desc(s[i], best_k & 15u, best_k >> 4);
+}
+
+// One workgroup of 256: the palette is the (up to) kChromaPalette most used
+// pairs (ties: the smaller k); palette_of[k] = 8 * slot or 0xFF, and the
+// byte-spread pair of each slot.
+__global__ __launch_bounds__(256) void chroma_palette_kernel(ChromaTables* ct) {
+  const uint32_t k = threadIdx.x;
+  const uint32_t n = ct->pair_hist[k];
+  uint32_t rank = 0;
+  for (uint32_t j = 0; j < 256; ++j) {
+    const uint32_t m = ct->pair_hist[j];
+    rank += (m > n) | ((m == n) & (j < k));
+  }
+  const bool in = n > 0 && rank < (uint32_t)kChromaPalette;
+  ct->palette_of[k] = in ? (uint8_t)(8u * rank) : (uint8_t)0xFFu;
+  if (in) {
+    ct->palette[2 * rank] = spread4(k & 15u);
+    ct->palette[2 * rank + 1] = spread4(k >> 4);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -339,7 +375,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
   {  // stage block masks, the mask-pair table and the run descriptors
     for (int i = t; i < 4096 / 16; i += blockDim.x)
       *(lds128_t)(uintptr_t)(kLdsBlocks + 16 * i) = reinterpret_cast<const u32x4*>(ct->blocks)[i];
-    for (int i = t; i < 256; i += blockDim.x) st64(kLdsPairs + 8 * i, spread4(i & 15u), spread4(i >> 4));
+    for (int i = t; i < kChromaPalette; i += blockDim.x) st64(kLdsPairs + 8 * i, ct->palette[2 * i], ct->palette[2 * i + 1]);
     for (int i = t; i < 131072 / 16; i += blockDim.x)
       *(lds128_t)(uintptr_t)(kLdsRuns + 16 * i) = reinterpret_cast<const u32x4*>(ct->runs)[i];
     for (int i = t; i < 256; i += blockDim.x) {
@@ -462,7 +498,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
           ba[i] = kLdsPairs + 8u * (c[i] >> 12);
 #else
           d[i] = ld16(kLdsRuns + 2u * c[i]);
-          ba[i] = kLdsPairs + 8u * ld8(kLdsBlocks + (c[i] >> 4));
+          ba[i] = kLdsPairs + ld8(kLdsBlocks + (c[i] >> 4));  // the block byte is the pair's offset
 #endif
         }
 #ifdef TRIK_AB_NO_LDS
@@ -657,7 +693,11 @@ int build_chroma_tables(const RangeTables* t, ChromaTables* ct, hipStream_t s) {
   hipLaunchKernelGGL(chroma_summary_kernel, dim3(256), dim3(256), 0, s, t, ct);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(chroma_block_kernel, dim3(4096 / 256), dim3(256), 0, s, ct);
+  e = hipMemsetAsync(ct->pair_hist, 0, sizeof(ct->pair_hist), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(chroma_block_kernel<false>, dim3(4096 / 256), dim3(256), 0, s, ct);
+  hipLaunchKernelGGL(chroma_palette_kernel, dim3(1), dim3(256), 0, s, ct);
+  hipLaunchKernelGGL(chroma_block_kernel<true>, dim3(4096 / 256), dim3(256), 0, s, ct);
   return hipGetLastError();
 }
 

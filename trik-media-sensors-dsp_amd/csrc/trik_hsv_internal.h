@@ -64,13 +64,21 @@ static_assert(2 * sizeof(StripeTables) <= 160 * 1024, "two workgroups per CU");
 //                 fast path's mask is Y <= b2 ? (Y < b1 ? M1 : M2) : 0; with
 //                 b1 > b2 + 1 the pixels b2 < Y < b1 go to the exact path
 //                 (a "window"), and kChromaExc sends both pixels there
-//   blocks[b]   : M1 | M2 << 4 (4-bit masks) of block b = c >> 4
 //   summary[c]  : builder scratch (run summary of the chroma's profile)
 constexpr uint32_t kChromaExc = 0x00FFu;  // b1 = 255, b2 = 0: the builder never makes this window
+//   blocks[b]   : final: 8 x the palette slot of block b's mask pair (the
+//                 hot kernel's LDS offset of the pair); builder scratch: the
+//                 pair k = M1 | M2 << 4 itself
+//   palette     : the byte-spread (M1, M2) of each palette slot; palette_of[k]
+//                 is 8 x the slot of pair k, or 0xFF; pair_hist: blocks per pair
+constexpr int kChromaPalette = 32;  // 8 x slot fits the block byte
 struct alignas(16) ChromaTables {
   uint16_t runs[65536];
   uint8_t blocks[4096];
   uint32_t summary[65536];
+  uint32_t pair_hist[256];
+  uint32_t palette[2 * kChromaPalette];
+  uint8_t palette_of[256];
 };
 
 PackedRange pack_range(const TRIK_VIDTRANSCODE_CV_InArgsAlg& r);
