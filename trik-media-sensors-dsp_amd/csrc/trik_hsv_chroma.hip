@@ -55,6 +55,7 @@ constexpr int kChunkWords = TRIK_CHROMA_CW;  // YUYV words per lane and row (8: 
 static_assert(kChunkWords == 4 || kChunkWords == 8, "chunk width");
 // steps per tile: byte counters P_i <= 2 * steps, O <= kChunkWords * steps
 constexpr int kMaxSteps = kChunkWords == 8 ? 31 : 63;
+static_assert((kChunkWords == 8 ? 4 : 2) * 2 * kMaxSteps <= 255, "flush group sums fit a byte");
 constexpr int kQFlush = 7;
 constexpr int kQueueCap = 128;  // entries per wave: < 64 waiting + <= 64 added by one word slot
 
@@ -561,20 +562,30 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         for (int i = 0; i < CW; i += 2) Q = Q + P[i] + P[i + 1];
         ++nb;
         if (nb == kQBlock || s + 1 == steps) {
-          const uint32_t T = Q - (uint32_t)nb * CumS;
-          Qa += T & 0x00FF00FFu;
-          Qb += (T >> 8) & 0x00FF00FFu;
-          Ba += (uint32_t)nb * CumA;
-          Bb += (uint32_t)nb * CumB;
-          CumS = 0;
-          CumA = 0;
-          CumB = 0;
+          // n * x for the block length n: a shift-add for full blocks (n is
+          // wave-uniform), a multiply only for a tile's last, partial block
+          auto flush = [&](auto times) {
+            const uint32_t T = Q - times(CumS);
+            Qa += T & 0x00FF00FFu;
+            Qb += (T >> 8) & 0x00FF00FFu;
+            Ba += times(CumA);
+            Bb += times(CumB);
+            // group sums of the pair counters stay below 256 per byte
+            // (kGroup * 2 * kMaxSteps <= 255), so one split per group
+            constexpr int kGroup = CW == 8 ? 4 : 2;
+            CumS = CumA = CumB = 0;
 #pragma unroll
-          for (int i = 0; i < CW; ++i) {
-            CumS += P[i];
-            CumA += P[i] & 0x00FF00FFu;
-            CumB += (P[i] >> 8) & 0x00FF00FFu;
-          }
+            for (int g0 = 0; g0 < CW; g0 += kGroup) {
+              uint32_t G = 0;
+#pragma unroll
+              for (int i = g0; i < g0 + kGroup; ++i) G += P[i];
+              CumS += G;
+              CumA += G & 0x00FF00FFu;
+              CumB += (G >> 8) & 0x00FF00FFu;
+            }
+          };
+          if (nb == kQBlock) flush([](uint32_t x) { return x * (uint32_t)kQBlock; });
+          else flush([&](uint32_t x) { return x * (uint32_t)nb; });
           Q = 0;
           nb = 0;
         }
