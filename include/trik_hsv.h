@@ -389,14 +389,22 @@ int32_t trik_hsv_batch_sums(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvFra
 /* Hot-kernel selection for trik_hsv_batch_sums / _process_batch / _masks
  * (process-wide; for tests and A/B runs).  TRIK_HSV_HOT_AUTO picks the
  * chroma-run kernel for batches of at least TRIK_HSV_CHROMA_MIN_PIXELS pixels
- * whose geometry it takes, the stripe kernel otherwise; the two give the same
+ * whose geometry it takes and whose range set sends at most
+ * TRIK_HSV_CHROMA_MAX_SHARE of the words to its exact path (see
+ * trik_hsv_chroma_share), the stripe kernel otherwise; the two give the same
  * results.  Returns the previous setting, or -1 for an unknown kind. */
 #define TRIK_HSV_HOT_AUTO 0
 #define TRIK_HSV_HOT_STRIPE 1
 #define TRIK_HSV_HOT_CHROMA 2
 #define TRIK_HSV_HOT_GENERIC 3
 #define TRIK_HSV_CHROMA_MIN_PIXELS (32 * 640 * 480)
+#define TRIK_HSV_CHROMA_MAX_SHARE 0.25
 int32_t trik_hsv_set_hot_kernel(int32_t kind);
+/* The chroma-run kernel's expected exact-path word share (uniform input) for
+ * the handle's current batched-sums range set (the maximum over its groups of
+ * 4 ranges), or -1 when its tables are not built yet.  Returns 0 or
+ * TRIK_IVIDTRANSCODE_EFAIL. */
+int32_t trik_hsv_chroma_share(TRIK_VIDTRANSCODE_CV_Handle handle, double* share);
 /* The kernel the last hot launch on this thread ran (TRIK_HSV_HOT_STRIPE,
  * _CHROMA or _GENERIC; 0 before any). */
 int32_t trik_hsv_last_hot_kernel(void);

@@ -2,11 +2,13 @@
 CPU oracle, bit-exact, through the C ABI with the kernel forced by
 trik_hsv.set_hot_kernel(HOT_CHROMA).
 
-The kernel resolves most YUYV words from per-chroma run descriptors and the
-rest ("exception" chromas, ~12 % at the bench's 4 ranges) from exact profile
-rows, so the cases below cover both paths: every (Y,U,V) triple, uniform and
-scene batches at the configs' shapes, several range groups, strided and
-padded frames, and the table rebuild when the range set changes.
+The kernel resolves most YUYV words from per-chroma run descriptors; the
+pixels inside a chroma's window, and both pixels of exception-code chromas,
+go to its exact path (6 % of words at the bench's 4 ranges, 60 % for the
+adversarial band sets below).  The cases cover both paths: every (Y,U,V)
+triple, uniform and scene batches at the configs' shapes, several range
+groups, strided and padded frames, the table rebuild when the range set
+changes, and the AUTO selector's exact-path-share guard.
 """
 import numpy as np
 import pytest
@@ -184,4 +186,50 @@ def test_auto_keeps_small_batches_on_stripe(torch_dev, hsv, detector):
         detector.process_batch(dev, 640, 480, 1280, LAYOUT_YUYV, [T0])
         assert hsv.last_hot_kernel() == hsv.HOT_STRIPE
     finally:
+        hsv.set_hot_kernel(prev)
+
+
+# range sets whose profiles have several separate runs per chroma: most words
+# reach the exact path (scripts/adversarial_ranges.py)
+S_BANDS = [(0, 359, 20, 25, 0, 100), (0, 359, 40, 45, 0, 100), (0, 359, 60, 65, 0, 100), (0, 359, 80, 85, 0, 100)]
+V_BANDS = [(0, 359, 0, 100, 20, 25), (0, 359, 0, 100, 40, 45), (0, 359, 0, 100, 60, 65), (0, 359, 0, 100, 80, 85)]
+
+
+@pytest.mark.parametrize("ranges", [S_BANDS, V_BANDS], ids=["s_bands", "v_bands"])
+def test_chroma_exhaustive_adversarial(torch_dev, detector, oracle_mod, chroma, ranges):
+    """Every (Y,U,V) triple through a range set that sends most words to the
+    exact path (many windows and exception-code chromas)."""
+    torch = torch_dev
+    frame, w, h, ll = exhaustive_yuyv_frame()
+    _, want = oracle_mod.frame(frame, w, h, ll, LAYOUT_YUYV, ranges, want_mask=True)
+    masks, sums = detector.batch_masks(_to_dev(torch, frame), w, h, ll, LAYOUT_YUYV, ranges)
+    assert chroma.last_hot_kernel() == chroma.HOT_CHROMA
+    assert detector.chroma_flagged_share() > 0.5
+    got = masks[0].cpu().numpy()
+    assert np.array_equal(got, want), f"{np.count_nonzero(got != want)} pixels differ"
+    assert sums[0].cpu().numpy().tolist() == sums_from_mask(want, len(ranges)).tolist()
+
+
+def test_auto_share_guard(torch_dev, hsv, oracle_mod):
+    """AUTO runs the chroma kernel for the bench ranges (share ~6 %) and the
+    stripe kernel for a range set whose exact-path share is above
+    TRIK_HSV_CHROMA_MAX_SHARE; both equal the oracle."""
+    torch = torch_dev
+    w, h, ll, n = 640, 480, 1280, 32  # TRIK_HSV_CHROMA_MIN_PIXELS
+    dev = torch.empty(n * h * ll, dtype=torch.uint8, device="cuda")
+    hsv.synth(dev, w, h, ll, LAYOUT_YUYV, 0, 0x7A1C, first_frame=9)
+    host = dev.cpu().numpy()
+    prev = hsv.set_hot_kernel(hsv.HOT_AUTO)
+    d = hsv.Detector()
+    try:
+        assert d.chroma_flagged_share() == -1.0
+        for ranges, kernel, lo, hi in ((BENCH_RANGES, hsv.HOT_CHROMA, 0.04, 0.08),
+                                       (S_BANDS, hsv.HOT_STRIPE, 0.5, 0.7)):
+            sums, _ = d.process_batch(dev, w, h, ll, LAYOUT_YUYV, ranges)
+            assert hsv.last_hot_kernel() == kernel
+            assert lo < d.chroma_flagged_share() < hi
+            want, _ = oracle_mod.batch(host, h * ll, n, w, h, ll, LAYOUT_YUYV, ranges, n_threads=8)
+            assert np.array_equal(sums.cpu().numpy(), want)
+    finally:
+        d.close()
         hsv.set_hot_kernel(prev)

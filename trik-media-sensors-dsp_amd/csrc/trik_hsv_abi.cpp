@@ -138,10 +138,12 @@ struct TableSet {
   StripeTables* h_stripe = nullptr;
   ChromaTables* d_chroma = nullptr;  // built on first use per range set (chroma-run kernel)
   bool chroma_built = false;
+  double chroma_share = -1.0;  // the builder's expected exact-path word share (max over groups)
   void release() {
     (void)hipFree(d_chroma);
     d_chroma = nullptr;
     chroma_built = false;
+    chroma_share = -1.0;
     (void)hipFree(d_tables);
     (void)hipHostFree(h_tables);
     (void)hipFree(d_stripe);
@@ -322,10 +324,21 @@ int32_t ensure_tables(TrikCvHandle* h, TableSet& t, const TRIK_VIDTRANSCODE_CV_I
 
 // The chroma-run kernel's tables for the current range set (built on the
 // device from the uploaded RangeTables, stream-ordered on s).
+// Also reads back the builder's expected exact-path share (one small
+// synchronous copy per range set).
 int32_t ensure_chroma(TableSet& t, int groups, hipStream_t s) {
   if (t.chroma_built) return 0;
   if (!t.d_chroma) HIP_TRY(hipMalloc(&t.d_chroma, sizeof(ChromaTables) * t.groups_cap));
-  for (int g = 0; g < groups; ++g) HIP_TRY(build_chroma_tables(t.d_tables + g, t.d_chroma + g, s));
+  double share = 0.0;
+  for (int g = 0; g < groups; ++g) {
+    HIP_TRY(build_chroma_tables(t.d_tables + g, t.d_chroma + g, s));
+    unsigned long long cost = 0;
+    HIP_TRY(hipMemcpyAsync(&cost, &t.d_chroma[g].flagged_cost, sizeof(cost), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const double sh = (double)cost / 4294967296.0;
+    if (sh > share) share = sh;
+  }
+  t.chroma_share = share;
   t.chroma_built = true;
   return 0;
 }
@@ -361,8 +374,12 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
     int e = hipErrorNotSupported;
     if ((choice == TRIK_HSV_HOT_CHROMA || (choice == TRIK_HSV_HOT_AUTO && big)) && chroma_geometry_ok(a)) {
       HIP_TRY(ensure_chroma(h->sums_tables, (n + kRangesPerLaunch - 1) / kRangesPerLaunch, s));
-      e = launch_chroma(a, h->sums_tables.d_chroma + g, masks != nullptr, s);
-      if (e == hipSuccess) g_last_hot = TRIK_HSV_HOT_CHROMA;
+      // AUTO keeps range sets whose profiles send too much to the exact path
+      // (many separate runs per chroma) on the stripe kernel
+      if (choice == TRIK_HSV_HOT_CHROMA || h->sums_tables.chroma_share <= TRIK_HSV_CHROMA_MAX_SHARE) {
+        e = launch_chroma(a, h->sums_tables.d_chroma + g, masks != nullptr, s);
+        if (e == hipSuccess) g_last_hot = TRIK_HSV_HOT_CHROMA;
+      }
     }
     if (e == hipErrorNotSupported && choice != TRIK_HSV_HOT_GENERIC) {
       e = launch_stripe(a, masks != nullptr, s);
@@ -877,6 +894,13 @@ extern "C" int32_t trik_hsv_set_hot_kernel(int32_t kind) {
 }
 
 extern "C" int32_t trik_hsv_last_hot_kernel(void) { return g_last_hot; }
+
+extern "C" int32_t trik_hsv_chroma_share(TRIK_VIDTRANSCODE_CV_Handle h, double* share) {
+  if (!h || !share) return fail(TRIK_IVIDTRANSCODE_EFAIL, "NULL handle or share");
+  std::lock_guard<std::mutex> lock(h->mu);
+  *share = h->sums_tables.chroma_built ? h->sums_tables.chroma_share : -1.0;
+  return 0;
+}
 
 extern "C" const char* trik_hsv_version(void) { return "trik-hsv-mi355x 0.1.0 (gfx950)"; }
 

@@ -257,6 +257,7 @@ __global__ __launch_bounds__(256) void chroma_block_kernel(ChromaTables* ct) {
   ct->blocks[b] = ct->palette_of[best_k];
 #pragma unroll
   for (int i = 0; i < 16; ++i) ct->runs[c0 + i] = (uint16_t)chroma_desc(s[i], best_k & 15u, best_k >> 4);
+  atomicAdd(&ct->flagged_cost, (unsigned long long)block_cost(best_k));
 }
 
 // One workgroup of 256: the palette is the (up to) kChromaPalette most used
@@ -705,6 +706,8 @@ int build_chroma_tables(const RangeTables* t, ChromaTables* ct, hipStream_t s) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(ct->pair_hist, 0, sizeof(ct->pair_hist), s);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(&ct->flagged_cost, 0, sizeof(ct->flagged_cost), s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(chroma_block_kernel<false>, dim3(4096 / 256), dim3(256), 0, s, ct);
   hipLaunchKernelGGL(chroma_palette_kernel, dim3(1), dim3(256), 0, s, ct);

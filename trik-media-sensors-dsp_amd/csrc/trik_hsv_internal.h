@@ -79,6 +79,10 @@ struct alignas(16) ChromaTables {
   uint32_t pair_hist[256];
   uint32_t palette[2 * kChromaPalette];
   uint8_t palette_of[256];
+  // sum over all chromas of the expected exact-path words per 65536 words
+  // (chroma_cost): / 2^32 = the expected share of words the exact path takes
+  // on uniform input; the host's AUTO selector reads it
+  unsigned long long flagged_cost;
 };
 
 PackedRange pack_range(const TRIK_VIDTRANSCODE_CV_InArgsAlg& r);

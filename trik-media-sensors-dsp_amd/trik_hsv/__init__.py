@@ -126,6 +126,15 @@ class Detector:
             raise TrikHsvError(rc, "trik_hsv_batch_sums")
         return sums
 
+    def chroma_flagged_share(self) -> float:
+        """The chroma-run kernel's expected exact-path word share for the
+        current batched-sums range set (-1 before its tables are built)."""
+        v = C.c_double()
+        rc = _lib.trik_hsv_chroma_share(self._h, C.byref(v))
+        if rc:
+            raise TrikHsvError(rc, "trik_hsv_chroma_share")
+        return v.value
+
     def batch_masks(self, frames, width, height, line_length, layout, ranges, *, n_frames=None,
                     frame_stride=None, stream=None):
         """Verification mode: returns (masks uint8 [N,H,W], sums int64 [N,T,3])."""

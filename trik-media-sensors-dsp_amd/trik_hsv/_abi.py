@@ -200,6 +200,7 @@ PROTOTYPES = {
     "trik_hsv_synth": ([C.POINTER(FrameBatch), i32, i32, u64, C.c_void_p], i32),
     "trik_hsv_set_hot_kernel": ([i32], i32),
     "trik_hsv_last_hot_kernel": ([], i32),
+    "trik_hsv_chroma_share": ([C.c_void_p, C.POINTER(C.c_double)], i32),
 }
 
 _lib = None
