@@ -260,26 +260,40 @@ void stripe_kernel(KernelArgs a, StripeGeom g) {
   }
 }
 
-bool geometry(const KernelArgs& a, StripeGeom& g) {
-  const int cpr = a.width >> 3;
-  if (cpr <= 0 || cpr > kMaxBlock || a.height <= 0) return false;
-  const int k = kMaxBlock / cpr;
-  const int steps_total = (a.height + k - 1) / k;
-  const int tiles = (steps_total + kMaxSteps - 1) / kMaxSteps;
-  g.cpr = cpr;
-  g.k = k;
-  g.tiles_per_frame = tiles;
-  g.steps = (steps_total + tiles - 1) / tiles;
-  g.n_tiles = (int64_t)tiles * a.n_frames;
-  return true;
-}
-
 int cu_count_stripe() {
   int dev = 0, n = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 256;
   if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
     return 256;
   return n;
+}
+
+// two workgroups per CU (LDS and VGPR budgets)
+int64_t stripe_slots() {
+  static int cus = 0;
+  if (!cus) cus = cu_count_stripe();
+  return 2LL * cus;
+}
+
+// Tiles of <= kMaxSteps steps; small batches split each frame into more
+// (shorter) tiles until the grid fills the chip's workgroup slots -- one VGA
+// frame is 40 one-step tiles instead of one 40-step tile on a single CU.
+bool geometry(const KernelArgs& a, StripeGeom& g, int64_t slots) {
+  const int cpr = a.width >> 3;
+  if (cpr <= 0 || cpr > kMaxBlock || a.height <= 0) return false;
+  const int k = kMaxBlock / cpr;
+  const int steps_total = (a.height + k - 1) / k;
+  int64_t tiles = (steps_total + kMaxSteps - 1) / kMaxSteps;
+  if (a.n_frames > 0 && tiles * a.n_frames < slots) {
+    const int64_t want = (slots + a.n_frames - 1) / a.n_frames;
+    tiles = want < steps_total ? want : steps_total;
+  }
+  g.cpr = cpr;
+  g.k = k;
+  g.steps = (int)((steps_total + tiles - 1) / tiles);
+  g.tiles_per_frame = (steps_total + g.steps - 1) / g.steps;
+  g.n_tiles = (int64_t)g.tiles_per_frame * a.n_frames;
+  return true;
 }
 
 template <int LAYOUT, int NR, bool MASKS>
@@ -293,10 +307,8 @@ int launch_t(const KernelArgs& a, const StripeGeom& g, hipStream_t s) {
     if (e != hipSuccess) return e;
     attr = true;
   }
-  static int cus = 0;
-  if (!cus) cus = cu_count_stripe();
   const int block = ((g.k * g.cpr + 63) / 64) * 64;
-  const int64_t slots = 2LL * cus;  // two workgroups per CU (LDS and VGPR budgets)
+  const int64_t slots = stripe_slots();
   const int64_t grid = g.n_tiles < slots ? g.n_tiles : slots;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(block), sizeof(StripeTables), s, a, g);
   return hipGetLastError();
@@ -317,7 +329,7 @@ int launch_nr(const KernelArgs& a, const StripeGeom& g, hipStream_t s) {
 
 int launch_stripe(const KernelArgs& a, bool write_masks, hipStream_t s) {
   StripeGeom g;
-  if (!geometry(a, g)) return hipErrorNotSupported;
+  if (!geometry(a, g, stripe_slots())) return hipErrorNotSupported;
   const int64_t need = a.layout == TRIK_HSV_LAYOUT_YUYV ? 16 : 8;
   if ((reinterpret_cast<uintptr_t>(a.frames) % need) || (a.frame_stride % need) ||
       (a.line_length % need))
