@@ -37,6 +37,9 @@ namespace {
 using namespace stripe_px;
 
 constexpr int kMaxBlock = 1024;
+constexpr uint32_t kLdsReduce = sizeof(StripeTables);          // u64 [16 waves][3 * 4]: flush_frame
+constexpr uint32_t kLdsStripe = kLdsReduce + 16 * 12 * 8;        // the dynamic LDS of one workgroup
+static_assert(2 * kLdsStripe <= 160 * 1024, "two workgroups per CU");
 constexpr int kMaxSteps = 63;  // byte counters: P_i <= 2*63, O <= 4*63 (a VGA frame is one 40-step tile)
 constexpr int kQFlush = 7;     // steps per Q block: block-relative sums <= 8*(1+...+7) = 224
 
@@ -71,15 +74,28 @@ __device__ __forceinline__ void wave_sums(uint32_t (&v)[N]) {
 // Wave-reduce the per-lane accumulators of one tile and add them to sums[frame].
 template <int NR>
 __device__ __forceinline__ void flush_frame(uint32_t (&acc)[3 * NR], int frame, const KernelArgs& a) {
+  // wave sums, then the workgroup's sum in LDS (64-bit: 16 waves' 32-bit
+  // sums may not fit 32 bits), then one atomic per value per workgroup -- a
+  // frame split into many short tiles (small batches) would otherwise pile
+  // 12 atomics per wave onto the same 12 addresses
   wave_sums<3 * NR>(acc);
+  typedef __attribute__((address_space(3))) unsigned long long* lds_u64_ptr;
+  const lds_u64_ptr red = (lds_u64_ptr)(uintptr_t)kLdsReduce;
+  const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 63) {
-    TrikHsvTargetSums* dst = a.sums + (int64_t)frame * a.sums_ranges + a.range_offset;
 #pragma unroll
-    for (int v = 0; v < 3 * NR; ++v)
-      if (acc[v])
-        atomicAdd(reinterpret_cast<unsigned long long*>(&dst[v / 3].points) + (v % 3),
-                  (unsigned long long)acc[v]);
+    for (int v = 0; v < 3 * NR; ++v) red[w * 3 * NR + v] = acc[v];
   }
+  __syncthreads();
+  if (threadIdx.x < 3 * NR) {
+    unsigned long long sum = 0;
+    for (int j = 0; j < (int)(blockDim.x >> 6); ++j) sum += red[j * 3 * NR + threadIdx.x];
+    if (sum) {
+      TrikHsvTargetSums* dst = a.sums + (int64_t)frame * a.sums_ranges + a.range_offset;
+      atomicAdd(reinterpret_cast<unsigned long long*>(&dst[threadIdx.x / 3].points) + (threadIdx.x % 3), sum);
+    }
+  }
+  __syncthreads();  // the slots are written again at the next tile's flush
 #pragma unroll
   for (int v = 0; v < 3 * NR; ++v) acc[v] = 0;
 }
@@ -303,14 +319,14 @@ int launch_t(const KernelArgs& a, const StripeGeom& g, hipStream_t s) {
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)sizeof(StripeTables));
+                                       (int)kLdsStripe);
     if (e != hipSuccess) return e;
     attr = true;
   }
   const int block = ((g.k * g.cpr + 63) / 64) * 64;
   const int64_t slots = stripe_slots();
   const int64_t grid = g.n_tiles < slots ? g.n_tiles : slots;
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(block), sizeof(StripeTables), s, a, g);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(block), kLdsStripe, s, a, g);
   return hipGetLastError();
 }
 
