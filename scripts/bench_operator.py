@@ -103,7 +103,7 @@ def main():
     out["blob"] = {"frames": lf, "ms": round(bl_ms, 4), "Mframes_per_s": round(lf / bl_ms / 1e3, 3),
                    "achieved_GBs": round(lf * lfb / (bl_ms / 1e3) / 1e9, 1),
                    "hbm_frac": round(lf * lfb / (bl_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                   "note": "blob_meta_kernel + blob_ccl_kernel (one wave per frame)"}
+                   "note": "bitmap (blob_chroma_meta_kernel for large batches, else blob_meta_kernel) + blob_ccl_kernel (one wave per frame)"}
     ldev_host = ldev[: 8 * lfb].cpu().numpy()
     del ldev
 

@@ -53,8 +53,12 @@ CASES = [("scene", 1, 0.0), ("scene", 2, 0.03), ("meta", 3, 0.5), ("meta", 4, 0.
          ("meta", 6, 0.0)]
 
 
+@pytest.mark.parametrize("hot", ["auto", "chroma"])
 @pytest.mark.parametrize("geom", GEOMS)
-def test_blob_batch_vs_oracle(hsv, oracle_mod, geom):
+def test_blob_batch_vs_oracle(hsv, oracle_mod, geom, hot):
+    """Both bitmap kernels: the stripe-arithmetic one (AUTO at these batch
+    sizes) and the chroma-run one (forced; it needs width % 16 and 16-byte
+    aligned lines, else the stripe-arithmetic one runs)."""
     import torch
 
     w, h, ll = geom
@@ -62,11 +66,39 @@ def test_blob_batch_vs_oracle(hsv, oracle_mod, geom):
     frames = _frames(oracle_mod, w, h, ll, cases)
     dev = torch.from_numpy(np.concatenate(frames)).cuda()
     det = hsv.Detector()
+    prev = hsv.set_hot_kernel(hsv.HOT_CHROMA if hot == "chroma" else hsv.HOT_AUTO)
     try:
         res = det.blob_batch(dev, w, h, ll, RED, meta=True, labels=True)
+        chroma_ok = hot == "chroma" and w % 16 == 0 and ll % 16 == 0
+        assert hsv.last_hot_kernel() == (hsv.HOT_CHROMA if chroma_ok else hsv.HOT_STRIPE)
         for i, fr in enumerate(frames):
             _check(oracle_mod, res, i, fr, w, h, ll, RED, (geom, cases[i]))
     finally:
+        hsv.set_hot_kernel(prev)
+        det.close()
+
+
+def test_blob_batch_auto_chroma_bitmap(hsv, oracle_mod):
+    """A batch past TRIK_HSV_CHROMA_MIN_PIXELS: AUTO builds the bitmap on the
+    chroma-run tables; scenes and bitmap-driven frames against the oracle,
+    for two ranges (the table rebuild when the sticky range changes)."""
+    import torch
+
+    w, h, ll = 640, 480, 640
+    cases = [("scene", 10 + i, 0.02 * (i % 3)) for i in range(20)] + \
+            [("meta", 40 + i, 0.05 + 0.1 * (i % 6)) for i in range(12)]
+    frames = _frames(oracle_mod, w, h, ll, cases)
+    dev = torch.from_numpy(np.concatenate(frames)).cuda()
+    det = hsv.Detector()
+    prev = hsv.set_hot_kernel(hsv.HOT_AUTO)
+    try:
+        for rng_hsv in (RED, (120, 40, 50, 50, 60, 40)):
+            res = det.blob_batch(dev, w, h, ll, rng_hsv, meta=True, labels=True)
+            assert hsv.last_hot_kernel() == hsv.HOT_CHROMA
+            for i, fr in enumerate(frames):
+                _check(oracle_mod, res, i, fr, w, h, ll, rng_hsv, (rng_hsv, cases[i]))
+    finally:
+        hsv.set_hot_kernel(prev)
         det.close()
 
 

@@ -563,6 +563,27 @@ int32_t blob_args(TrikCvHandle* h, const TrikHsvFrameBatch& b, const TRIK_VIDTRA
   return 0;
 }
 
+// The multi-blob sensor: the metapixel bitmap on the chroma-run tables of the
+// sticky range when the hot-kernel setting allows it (AUTO: batches of at
+// least TRIK_HSV_CHROMA_MIN_PIXELS whose exact-path share is low), else the
+// stripe-arithmetic kernel inside launch_blob; then the clusterer.
+int32_t run_blob(TrikCvHandle* h, BlobArgs& ba, hipStream_t s) {
+  const int choice = g_hot_kernel.load();
+  const bool big = (int64_t)ba.n_frames * ba.width * ba.height >= (int64_t)TRIK_HSV_CHROMA_MIN_PIXELS;
+  ba.meta_ready = 0;
+  g_last_hot = TRIK_HSV_HOT_STRIPE;
+  if ((choice == TRIK_HSV_HOT_CHROMA || (choice == TRIK_HSV_HOT_AUTO && big)) && blob_chroma_ok(ba)) {
+    HIP_TRY(ensure_chroma(h->single_tables, 1, s));
+    if (choice == TRIK_HSV_HOT_CHROMA || h->single_tables.chroma_share <= TRIK_HSV_CHROMA_MAX_SHARE) {
+      HIP_TRY(launch_blob_meta_chroma(ba, h->single_tables.d_chroma, h->single_tables.d_tables, s));
+      ba.meta_ready = 1;
+      g_last_hot = TRIK_HSV_HOT_CHROMA;
+    }
+  }
+  HIP_TRY(launch_blob(ba, s));
+  return 0;
+}
+
 AutoRangeArgs auto_range_args(const TrikHsvFrameBatch& b, uint16_t* out) {
   AutoRangeArgs a;
   a.frames = static_cast<const uint8_t*>(b.frames);
@@ -765,7 +786,8 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
           BlobArgs ba;
           r = blob_args(h, b, h->blob_range, nullptr, nullptr, nullptr, nullptr, nullptr, h->stream, ba);
           if (r) return r;
-          HIP_TRY(launch_blob(ba, h->stream));
+          r = run_blob(h, ba, h->stream);
+          if (r) return r;
           if (out_ptr && out_size > 0) {  // preview: set metapixels, guide lines, target marks
             const size_t pb = (size_t)out_size;
             r = grow(h->d_preview, h->d_preview_cap, pb);
@@ -1083,7 +1105,8 @@ extern "C" int32_t trik_hsv_blob_batch(TRIK_VIDTRANSCODE_CV_Handle h, const Trik
   BlobArgs ba;
   r = blob_args(h, *b, blob_range_args(*hsv), targets, top, meta, labels, n_labels, s, ba);
   if (r) return r;
-  HIP_TRY(launch_blob(ba, s));
+  r = run_blob(h, ba, s);
+  if (r) return r;
   if (!h->tables_busy) HIP_TRY(hipEventCreateWithFlags(&h->tables_busy, hipEventDisableTiming));
   HIP_TRY(hipEventRecord(h->tables_busy, s));
   if (!h->blob_busy) HIP_TRY(hipEventCreateWithFlags(&h->blob_busy, hipEventDisableTiming));

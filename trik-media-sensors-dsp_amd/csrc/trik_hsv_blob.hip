@@ -450,7 +450,7 @@ int launch_blob(const BlobArgs& a, hipStream_t s) {
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       cus = 256;
   }
-  if (total > 0) {
+  if (total > 0 && !a.meta_ready) {
     MetaGeom g;
     g.per_frame = make_div((uint32_t)(bw * bh));
     g.per_row = make_div((uint32_t)bw);

@@ -662,6 +662,140 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// The ov7670 multi-blob sensor's metapixel bitmap on the chroma-run tables
+// ---------------------------------------------------------------------------
+// BMB:171-190 / CLU:185-186: a metapixel (4x4 pixels) is set when more than 2
+// of its pixels are in the sticky range.  Same per-word fast path and exact
+// path as chroma_kernel, for one range: a lane takes an item = (frame,
+// metapixel row, 16-pixel column chunk) -- four rows of 8 words, four
+// metapixels -- and counts per metapixel; flagged words are queued per wave
+// with their owner lane and metapixel, and the drain adds their exact bits to
+// the owner's byte-packed counter word in LDS, which the owner adds before it
+// writes the four flags.
+constexpr uint32_t kLdsBlobCounts = kLdsQueues + 16 * kQueueCap * 8;  // u32 [1024]: 4 byte counts per lane
+constexpr uint32_t kLdsBlobBytes = kLdsBlobCounts + 4 * kMaxBlock;
+static_assert(kLdsBlobBytes <= 160 * 1024, "blob meta LDS image");
+
+struct BlobChromaGeom {
+  FastDiv per_frame;  // bh * cpr items per frame
+  FastDiv per_row;    // cpr items per metapixel row
+  uint32_t total;     // n_frames * bh * cpr
+  int32_t bw, bh;
+};
+
+__global__ __launch_bounds__(kMaxBlock) void blob_chroma_meta_kernel(BlobArgs a, BlobChromaGeom g,
+                                                                      const ChromaTables* ct,
+                                                                      const RangeTables* rt) {
+  const int t = threadIdx.x;
+  {  // the chroma kernel's tables (one range), zeroed count words
+    for (int i = t; i < 4096 / 16; i += blockDim.x)
+      *(lds128_t)(uintptr_t)(kLdsBlocks + 16 * i) = reinterpret_cast<const u32x4*>(ct->blocks)[i];
+    for (int i = t; i < kChromaPalette; i += blockDim.x) st64(kLdsPairs + 8 * i, ct->palette[2 * i], ct->palette[2 * i + 1]);
+    for (int i = t; i < 131072 / 16; i += blockDim.x)
+      *(lds128_t)(uintptr_t)(kLdsRuns + 16 * i) = reinterpret_cast<const u32x4*>(ct->runs)[i];
+    for (int i = t; i < 256; i += blockDim.x) {
+      *(lds16_t)(uintptr_t)(kLdsLut43 + 2 * i) = rt->lut43[i];
+      *(lds16_t)(uintptr_t)(kLdsLut255 + 2 * i) = rt->lut255[i];
+      *(lds8_t)(uintptr_t)(kLdsHue + i) = rt->hue[i];
+      *(lds8_t)(uintptr_t)(kLdsSat + i) = rt->smask[i];
+      *(lds8_t)(uintptr_t)(kLdsVal + i) = rt->vmask[i];
+    }
+    *(lds32_t)(uintptr_t)(kLdsBlobCounts + 4u * (uint32_t)t) = 0u;
+  }
+  __syncthreads();
+  const int lane = t & 63;
+  const uint32_t qbase_s = __builtin_amdgcn_readfirstlane(kLdsQueues + (uint32_t)(t >> 6) * (kQueueCap * 8));
+  const uint32_t wave0 = (uint32_t)(t & ~63);
+  const uint32_t my_counts = kLdsBlobCounts + 4u * (uint32_t)t;
+  const int64_t ll = a.line_length, plane = (int64_t)a.height * a.line_length;
+  int qn = 0;
+  // One drain round: lanes 0..take-1 resolve queue entries 0..take-1 exactly
+  // and add their bits to the owner's counter word; the rest moves up.
+  auto drain = [&](int take) {
+    if (lane < take) {
+      const u32x2 ent = ld64(qbase_s + 8u * (uint32_t)lane);
+      const uint32_t w = ent.x;
+      const uint32_t d = ld16(kLdsRuns + 2u * chroma_of(w));
+      const uint32_t lo = d & 0xFFu, hi = d >> 8, Y0 = w & 0xFFu, Y1 = (w >> 16) & 0xFFu;
+      const bool xw = d == kChromaExc;
+      const bool f0 = xw | ((Y0 < lo) & (Y0 > hi)), f1 = xw | ((Y1 < lo) & (Y1 > hi));
+      const uint32_t n = (f0 ? exact_mask<0>(w) & 1u : 0u) + (f1 ? exact_mask<1>(w) & 1u : 0u);
+      if (n) {
+        const uint32_t owner = wave0 + (ent.y & 63u), j = ent.y >> 6;
+        __hip_atomic_fetch_add((__attribute__((address_space(3))) uint32_t*)(uintptr_t)(kLdsBlobCounts + 4u * owner),
+                               n << (8u * j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    const int rest = qn - take;
+    if (rest > 0) {
+      u32x2 mv = {0u, 0u};
+      if (lane < rest) mv = ld64(qbase_s + 8u * (uint32_t)(take + lane));
+      __builtin_amdgcn_wave_barrier();
+      if (lane < rest) st64(qbase_s + 8u * (uint32_t)lane, mv.x, mv.y);
+    }
+    qn = rest;
+  };
+  for (uint32_t base = blockIdx.x * (uint32_t)kMaxBlock; base < g.total; base += gridDim.x * (uint32_t)kMaxBlock) {
+    const uint32_t item = base + (uint32_t)t;
+    const bool valid = item < g.total;
+    const uint64_t vm = __builtin_amdgcn_ballot_w64(valid);
+    const uint32_t it = valid ? item : 0u;
+    const uint32_t f = fdiv(it, g.per_frame), rem = it - f * g.per_frame.d;
+    const uint32_t mr = fdiv(rem, g.per_row), ch = rem - mr * g.per_row.d;
+    const uint8_t* p = a.frames + (int64_t)f * a.frame_stride + (int64_t)(4 * mr) * ll + 16 * (int64_t)ch;
+    uint32_t cnt[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint4 vy = *reinterpret_cast<const uint4*>(p + r * ll);
+      const uint4 vc = *reinterpret_cast<const uint4*>(p + r * ll + plane);
+      const uint32_t yy[4] = {vy.x, vy.y, vy.z, vy.w}, cc[4] = {vc.x, vc.y, vc.z, vc.w};
+      uint32_t w[8], d[8], ba[8];
+      u32x2 mm[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) stripe_px::ov7670_words(yy[k], cc[k], w[2 * k], w[2 * k + 1]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t c = chroma_of(w[i]);
+        d[i] = ld16(kLdsRuns + 2u * c);
+        ba[i] = kLdsPairs + ld8(kLdsBlocks + (c >> 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) mm[i] = ld64(ba[i]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(d[i]));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        uint32_t e0, e1;
+        uint64_t q0, q1;
+        select2(w[i], d[i], mm[i].x, mm[i].y, vm, e0, e1, q0, q1);
+        cnt[i >> 1] += e0 + e1;  // one range: the spread masks are 0 or 1
+        const uint64_t bal = q0 | q1;
+        const uint32_t idx =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        if (__builtin_amdgcn_inverse_ballot_w64(bal)) {
+          const uint32_t qa = __builtin_amdgcn_readfirstlane(qbase_s + 8u * (uint32_t)qn) + 8u * idx;
+          *(lds32_t)(uintptr_t)qa = w[i];
+          *(lds32_t)(uintptr_t)(qa + 4u) = (uint32_t)lane | ((uint32_t)(i >> 1) << 6);
+        }
+        qn += __builtin_popcountll(bal);
+        if (qn >= 64) drain(64);
+      }
+    }
+    while (qn > 0) drain(qn < 64 ? qn : 64);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t extra = *(lds32_t)(uintptr_t)my_counts;
+    *(lds32_t)(uintptr_t)my_counts = 0u;
+    if (valid) {
+      uint32_t flags = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) flags |= (cnt[j] + ((extra >> (8 * j)) & 0xFFu) > 2u ? 1u : 0u) << (8 * j);
+      *reinterpret_cast<uint32_t*>(a.meta + ((int64_t)f * g.bh + mr) * g.bw + 4 * (int64_t)ch) = flags;
+    }
+  }
+}
+
 int cu_count() {
   int dev = 0, n = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 256;
@@ -758,6 +892,39 @@ int launch_chroma(const KernelArgs& a, const ChromaTables* ct, bool write_masks,
                        : launch_nr<TRIK_HSV_LAYOUT_YUYV, false>(a, g, ct, s);
   return write_masks ? launch_nr<TRIK_HSV_LAYOUT_OV7670, true>(a, g, ct, s)
                      : launch_nr<TRIK_HSV_LAYOUT_OV7670, false>(a, g, ct, s);
+}
+
+
+bool blob_chroma_ok(const BlobArgs& a) {
+  return a.width > 0 && a.width % 16 == 0 && a.height % 4 == 0 && a.line_length % 16 == 0 &&
+         (reinterpret_cast<uintptr_t>(a.frames) % 16) == 0 && (a.n_frames <= 1 || a.frame_stride % 16 == 0);
+}
+
+int launch_blob_meta_chroma(const BlobArgs& a, const ChromaTables* ct, const RangeTables* rt, hipStream_t s) {
+  if (!blob_chroma_ok(a)) return hipErrorNotSupported;
+  const int bw = a.width >> 2, bh = a.height >> 2, cpr = a.width >> 4;
+  const int64_t total = (int64_t)a.n_frames * bh * cpr;
+  if (total <= 0) return hipSuccess;
+  if (total >= (1ll << 31)) return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(blob_chroma_meta_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBlobBytes);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  static int cus = 0;
+  if (!cus) cus = cu_count();
+  BlobChromaGeom g;
+  g.per_frame = make_div((uint32_t)(bh * cpr));
+  g.per_row = make_div((uint32_t)cpr);
+  g.total = (uint32_t)total;
+  g.bw = bw;
+  g.bh = bh;
+  const int64_t blocks = (total + kMaxBlock - 1) / kMaxBlock;
+  hipLaunchKernelGGL(blob_chroma_meta_kernel, dim3((unsigned)(blocks < cus ? blocks : cus)), dim3(kMaxBlock),
+                     kLdsBlobBytes, s, a, g, ct, rt);
+  return hipGetLastError();
 }
 
 }  // namespace trik_hsv

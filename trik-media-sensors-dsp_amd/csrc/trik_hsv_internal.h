@@ -188,12 +188,19 @@ struct BlobArgs {
   int32_t* top;              // [n][8][3]: size, sum_x, sum_y of the 8 largest clusters
   int32_t* n_labels;         // optional [n]
   int32_t meta_lds = 0;      // set by launch_blob: the bitmap staged in LDS
+  int32_t meta_ready = 0;    // the bitmap is already written (launch_blob_meta_chroma)
 };
 // Labels a frame can need: seeds are pairwise non-adjacent in the 8-neighbourhood
 // (a metapixel next to an earlier set one is never a seed), so at most
 // ceil(bw/2) * ceil(bh/2) of them, plus the background label 0.
 inline int64_t blob_max_labels(int bw, int bh) { return (int64_t)((bw + 1) / 2) * ((bh + 1) / 2) + 1; }
 int launch_blob(const BlobArgs& a, hipStream_t s);
+// The metapixel bitmap on the chroma-run tables of the sticky range (ct, rt:
+// its ChromaTables and RangeTables); hipErrorNotSupported when the geometry
+// needs the generic kernel (width % 16, 16-byte aligned frames and lines).
+// launch_blob with a.meta_from_chroma set then runs only the clusterer.
+bool blob_chroma_ok(const BlobArgs& a);
+int launch_blob_meta_chroma(const BlobArgs& a, const ChromaTables* ct, const RangeTables* rt, hipStream_t s);
 // guide lines + a 3x3 mark per kept target (OSEQ:548-580), from BlobArgs.top
 int launch_blob_overlay(const PreviewArgs& a, const int32_t* top, hipStream_t s);
 
