@@ -225,3 +225,22 @@ def test_blob_batch_zero_size_frames(hsv):
         assert not res["targets"].any() and not res["top"].any() and not res["n_labels"].any()
     finally:
         det.close()
+
+
+def test_blob_batch_large_from_l2(hsv, oracle_mod):
+    """A batch of >= 2 x CUs frames: the clusterer reads the bitmap from L2
+    instead of staging it in LDS (more frames resident per CU); small frames
+    with random bitmaps of several densities, every frame against the oracle."""
+    import torch
+
+    w, h, ll, n = 64, 32, 64, 520
+    cases = [("meta", 1000 + i, (0.05, 0.3, 0.55, 0.8)[i % 4]) for i in range(n)]
+    frames = _frames(oracle_mod, w, h, ll, cases)
+    dev = torch.from_numpy(np.concatenate(frames)).cuda()
+    det = hsv.Detector()
+    try:
+        res = det.blob_batch(dev, w, h, ll, RED, meta=True, labels=True)
+        for i, fr in enumerate(frames):
+            _check(oracle_mod, res, i, fr, w, h, ll, RED, cases[i])
+    finally:
+        det.close()
