@@ -221,8 +221,20 @@ __global__ __launch_bounds__(kRangeBlock) void auto_range_kernel(AutoRangeArgs a
   const int zw = c1 - c0, zh = r1 - r0;
   const int64_t zn = zw > 0 && zh > 0 ? (int64_t)zw * zh : 0;
   const uint8_t* fr = a.frames + (int64_t)f * a.frame_stride;
-  for (int64_t i = tid; i < zn; i += blockDim.x) {
-    const int row = r0 + (int)(i / zw), col = c0 + (int)(i % zw);
+  // the zone in scan order, thread tid taking pixels tid, tid + block, ...:
+  // (row, col) advanced incrementally (no division per pixel)
+  auto zone = [&](auto fn) {
+    if (zn <= 0) return;
+    const uint32_t zwu = (uint32_t)zw, sq = (uint32_t)kRangeBlock / zwu, sr = (uint32_t)kRangeBlock % zwu;
+    uint32_t zr = (uint32_t)tid / zwu, zc = (uint32_t)tid % zwu;
+    for (uint32_t i = (uint32_t)tid; i < (uint32_t)zn; i += kRangeBlock) {
+      fn(r0 + (int)zr, c0 + (int)zc);
+      zc += sr;
+      zr += sq;
+      if (zc >= zwu) { zc -= zwu; ++zr; }
+    }
+  };
+  zone([&](int row, int col) {
     uint32_t hv[3];
     hsv_bytes(fr, a, row, col, l43, l255, hv);
     const uint32_t pos = (uint32_t)((int64_t)row * a.width + col);  // scan order of s_rgb888hsv
@@ -231,7 +243,7 @@ __global__ __launch_bounds__(kRangeBlock) void auto_range_kernel(AutoRangeArgs a
       atomicAdd(&cnt[wave][k][hv[k]], 1u);
       if (!kTwoPass) atomicMax(&lst[kTwoPass ? 0 : wave][k][hv[k]], pos);
     }
-  }
+  });
   __syncthreads();
   // merge the waves: counts add, last positions take the maximum
   for (int i = tid; i < 3 * 256; i += blockDim.x) {
@@ -246,15 +258,14 @@ __global__ __launch_bounds__(kRangeBlock) void auto_range_kernel(AutoRangeArgs a
   }
   __syncthreads();
   if (kTwoPass) {
-    for (int64_t i = tid; i < zn; i += blockDim.x) {
-      const int row = r0 + (int)(i / zw), col = c0 + (int)(i % zw);
+    zone([&](int row, int col) {
       uint32_t hv[3];
       hsv_bytes(fr, a, row, col, l43, l255, hv);
       const uint32_t pos = (uint32_t)((int64_t)row * a.width + col);
 #pragma unroll
       for (int k = 0; k < 3; ++k)
         if (cnt[0][k][hv[k]] == best_n[k]) atomicMax(&lst[0][k][hv[k]], pos);
-    }
+    });
     __syncthreads();
   }
   for (int i = tid; i < 3 * 256; i += blockDim.x) {
