@@ -186,6 +186,27 @@ __device__ __forceinline__ void hsv_bytes(const uint8_t* fr, const AutoRangeArgs
   hsv[2] = (uint32_t)mx;
 }
 
+// One H (or S, V) value into a wave's histogram.  Same-bin LDS atomics of one
+// wave serialise lane by lane, and the zone of a ball is mostly one value: the
+// bin of the first active lane's value takes ONE atomic for all lanes holding
+// it (count = their number, last position = the highest such lane's, i.e. the
+// latest in scan order); the other lanes add their own.
+template <bool kCount, bool kLast>
+__device__ __forceinline__ void bin_add(uint32_t* cnt, uint32_t* lst, uint32_t v, uint32_t pos) {
+  // one peeled value per call: a second round costs more than it saves
+  // (4096 frames, scripts/range_time.py: none 0.78 ms, one 0.51, three 0.74)
+  const uint32_t v0 = __builtin_amdgcn_readfirstlane(v);
+  const unsigned long long m = __ballot(v == v0);
+  const uint32_t p0 = kLast ? (uint32_t)__builtin_amdgcn_readlane((int)pos, 63 - __clzll(m)) : 0u;
+  if (v != v0) {
+    if (kCount) atomicAdd(&cnt[v], 1u);
+    if (kLast) atomicMax(&lst[v], pos);
+  } else if (__lane_id() == (unsigned)(__ffsll((long long)m) - 1)) {
+    if (kCount) atomicAdd(&cnt[v0], (uint32_t)__popcll(m));
+    if (kLast) atomicMax(&lst[v0], p0);
+  }
+}
+
 // Per-wave sub-histograms (same-bin LDS atomics contend only within a wave).
 // kTwoPass = false: one pass records counts and last positions per value.
 // kTwoPass = true: pass 1 counts; pass 2 records the last position of the
@@ -239,10 +260,7 @@ __global__ __launch_bounds__(kRangeBlock) void auto_range_kernel(AutoRangeArgs a
     hsv_bytes(fr, a, row, col, l43, l255, hv);
     const uint32_t pos = (uint32_t)((int64_t)row * a.width + col);  // scan order of s_rgb888hsv
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      atomicAdd(&cnt[wave][k][hv[k]], 1u);
-      if (!kTwoPass) atomicMax(&lst[kTwoPass ? 0 : wave][k][hv[k]], pos);
-    }
+    for (int k = 0; k < 3; ++k) bin_add<true, !kTwoPass>(cnt[wave][k], lst[kTwoPass ? 0 : wave][k], hv[k], pos);
   });
   __syncthreads();
   // merge the waves: counts add, last positions take the maximum
@@ -264,7 +282,7 @@ __global__ __launch_bounds__(kRangeBlock) void auto_range_kernel(AutoRangeArgs a
       const uint32_t pos = (uint32_t)((int64_t)row * a.width + col);
 #pragma unroll
       for (int k = 0; k < 3; ++k)
-        if (cnt[0][k][hv[k]] == best_n[k]) atomicMax(&lst[0][k][hv[k]], pos);
+        if (cnt[0][k][hv[k]] == best_n[k]) bin_add<false, true>(cnt[0][k], lst[0][k], hv[k], pos);
     });
     __syncthreads();
   }
