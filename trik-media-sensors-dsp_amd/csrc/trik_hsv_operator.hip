@@ -51,6 +51,9 @@ __constant__ Luts c_luts = make_luts();
 // per-pixel arithmetic (phase1 also yields the clamped colour); with
 // a.meta set (the multi-blob preview) detection is the metapixel flag and no
 // tables are staged.  Every byte of the out_h x out_ll preview is written.
+#ifndef TRIK_PREVIEW_Q
+#define TRIK_PREVIEW_Q 2
+#endif
 struct PreviewGeom {
   FastDiv per_frame;  // out_h * quads per row
   FastDiv per_row;    // quads per row
@@ -72,45 +75,85 @@ void preview_gather_kernel(PreviewArgs a, PreviewGeom g) {
   const uint32_t m43_lane = (uint32_t)offsetof(StripeTables, m43) + ((t % kM43Copies) << 2);
   const uint32_t qpr = g.per_row.d;
   const int64_t ll = a.line_length;
-  for (uint32_t i = blockIdx.x * blockDim.x + t; i < g.total; i += gridDim.x * blockDim.x) {
-    const uint32_t f = fdiv(i, g.per_frame), rem = i - f * g.per_frame.d;
-    const uint32_t r = fdiv(rem, g.per_row), q = rem - r * qpr;
-    const uint8_t* fr = a.frames + (int64_t)f * a.frame_stride;
-    const int sr = a.last_row[r];
-    uint32_t v[2] = {0u, 0u};
+  // kQ output groups per thread, 64 apart (each load and store instruction of
+  // a wave stays on consecutive groups), in phases (positions, map loads, frame
+  // loads, arithmetic, stores) so that a thread's loads are in flight together:
+  // the loop is bound by the map -> frame -> LDS chain, not by bytes
+  constexpr int kQ = TRIK_PREVIEW_Q;
+  const uint32_t lane = t & 63u, wave_step = (gridDim.x * blockDim.x) >> 6;
+  const uint32_t n_chunks = (g.total + 64u * kQ - 1) / (64u * kQ);
+  for (uint32_t ch = (blockIdx.x * blockDim.x + t) >> 6; ch < n_chunks; ch += wave_step) {
+    uint32_t ff[kQ], rr[kQ], qq[kQ];
+    bool ok[kQ];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int c = 2 * (int)q + k;
-      if (c >= a.out_w || sr < 0) continue;
-      const int sc = a.last_col[c];
-      if (sc < 0) continue;
-      uint32_t w;  // the pixel as a YUYV word with its Y in byte 0
-      if (a.layout == TRIK_HSV_LAYOUT_YUYV && a.aligned4) {
-        w = *reinterpret_cast<const uint32_t*>(fr + (int64_t)sr * ll + 4 * (sc >> 1));
-        if (sc & 1) w = __builtin_amdgcn_perm(w, w, 0x03020102u);
-      } else {
-        int Y, U, V;
-        fetch_yuv(fr, a.height, a.line_length, a.layout, sr, sc, Y, U, V);
-        w = (uint32_t)Y | ((uint32_t)U << 8) | ((uint32_t)V << 24);
-      }
-      const Phase1 p = phase1<0>(w, w ^ 0xFF00FF00u, m43_lane);
-      uint32_t det;
-      if (a.meta) {
-        det = a.meta[((int64_t)f * (a.height >> 2) + (sr >> 2)) * (a.width >> 2) + (sc >> 2)];
-      } else {
-        const uint32_t m = lds_u32(p.m43_addr), sv = lds_u8(p.sv_addr);
-        det = combine(lds_u32(phase2_addr(m, p, hue_lane)), sv) & 1u;
-      }
-      const uint32_t rgb = det ? 0x00ffffu : p.rgb888;
-      v[k] = ((rgb >> 19) & 0x001fu) | ((rgb >> 5) & 0x07e0u) | ((rgb << 8) & 0xf800u);
+    for (int u = 0; u < kQ; ++u) {
+      const uint32_t i = ch * 64u * kQ + 64u * u + lane;
+      ok[u] = i < g.total;
+      ff[u] = fdiv(i, g.per_frame);
+      const uint32_t rem = i - ff[u] * g.per_frame.d;
+      rr[u] = fdiv(rem, g.per_row);
+      qq[u] = rem - rr[u] * qpr;
     }
-    uint8_t* row = a.previews + (int64_t)f * a.preview_stride + (int64_t)r * a.out_ll;
-    const int b0 = 4 * (int)q;
-    if (a.aligned4 && b0 + 4 <= a.out_ll) {
-      *reinterpret_cast<uint32_t*>(row + b0) = v[0] | (v[1] << 16);
-    } else {
-      const uint8_t bytes[4] = {(uint8_t)v[0], (uint8_t)(v[0] >> 8), (uint8_t)v[1], (uint8_t)(v[1] >> 8)};
-      for (int k = 0; k < 4 && b0 + k < a.out_ll; ++k) row[b0 + k] = bytes[k];
+    int sr[kQ], sc[kQ][2];
+#pragma unroll
+    for (int u = 0; u < kQ; ++u) {
+      sr[u] = ok[u] ? a.last_row[rr[u]] : -1;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int c = 2 * (int)qq[u] + k;
+        sc[u][k] = ok[u] && c < a.out_w ? a.last_col[c] : -1;
+      }
+    }
+    uint32_t w[kQ][2];  // each pixel as a YUYV word with its Y in byte 0
+#pragma unroll
+    for (int u = 0; u < kQ; ++u) {
+      const uint8_t* fr = a.frames + (int64_t)ff[u] * a.frame_stride;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        w[u][k] = 0u;
+        if (sr[u] < 0 || sc[u][k] < 0) continue;
+        if (a.layout == TRIK_HSV_LAYOUT_YUYV && a.aligned4) {
+          w[u][k] = *reinterpret_cast<const uint32_t*>(fr + (int64_t)sr[u] * ll + 4 * (sc[u][k] >> 1));
+        } else {
+          int Y, U, V;
+          fetch_yuv(fr, a.height, a.line_length, a.layout, sr[u], sc[u][k], Y, U, V);
+          w[u][k] = (uint32_t)Y | ((uint32_t)U << 8) | ((uint32_t)V << 24);
+        }
+      }
+    }
+    uint32_t out[kQ];
+#pragma unroll
+    for (int u = 0; u < kQ; ++u) {
+      uint32_t v[2] = {0u, 0u};
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        if (sr[u] < 0 || sc[u][k] < 0) continue;
+        uint32_t x = w[u][k];
+        if (a.layout == TRIK_HSV_LAYOUT_YUYV && a.aligned4 && (sc[u][k] & 1))
+          x = __builtin_amdgcn_perm(x, x, 0x03020102u);
+        const Phase1 p = phase1<0>(x, x ^ 0xFF00FF00u, m43_lane);
+        uint32_t det;
+        if (a.meta) {
+          det = a.meta[((int64_t)ff[u] * (a.height >> 2) + (sr[u] >> 2)) * (a.width >> 2) + (sc[u][k] >> 2)];
+        } else {
+          const uint32_t m = lds_u32(p.m43_addr), sv = lds_u8(p.sv_addr);
+          det = combine(lds_u32(phase2_addr(m, p, hue_lane)), sv) & 1u;
+        }
+        const uint32_t rgb = det ? 0x00ffffu : p.rgb888;
+        v[k] = ((rgb >> 19) & 0x001fu) | ((rgb >> 5) & 0x07e0u) | ((rgb << 8) & 0xf800u);
+      }
+      out[u] = v[0] | (v[1] << 16);
+    }
+#pragma unroll
+    for (int u = 0; u < kQ; ++u) {
+      if (!ok[u]) continue;
+      uint8_t* row = a.previews + (int64_t)ff[u] * a.preview_stride + (int64_t)rr[u] * a.out_ll;
+      const int b0 = 4 * (int)qq[u];
+      if (a.aligned4 && b0 + 4 <= a.out_ll) {
+        *reinterpret_cast<uint32_t*>(row + b0) = out[u];
+      } else {
+        for (int k = 0; k < 4 && b0 + k < a.out_ll; ++k) row[b0 + k] = (uint8_t)(out[u] >> (8 * k));
+      }
     }
   }
 }
@@ -330,7 +373,7 @@ static int launch_gather(const PreviewArgs& a, hipStream_t s) {
   g.per_frame = make_div((uint32_t)(a.out_h * qpr));
   g.per_row = make_div((uint32_t)qpr);
   g.total = (uint32_t)total;
-  const int64_t blocks = (total + 1023) / 1024, slots = 2LL * cus;
+  const int64_t blocks = (total + 1024LL * TRIK_PREVIEW_Q - 1) / (1024LL * TRIK_PREVIEW_Q), slots = 2LL * cus;
   hipLaunchKernelGGL(preview_gather_kernel, dim3((unsigned)(blocks < slots ? blocks : slots)), dim3(1024),
                      a.meta ? 0 : sizeof(StripeTables), s, a, g);
   return hipGetLastError();
