@@ -47,6 +47,10 @@ GEOMS = [
     (320, 240, 704, 160, 120, 333, LAYOUT_YUYV),
     (256, 240, 512, 100, 200, 200, LAYOUT_YUYV),
     (320, 240, 320, 160, 120, 320, LAYOUT_OV7670),
+    # upscaled (output pixels nobody writes: -1 in the maps), and maps too
+    # large for the gather kernel's LDS (out_w + out_h > 1536: read from memory)
+    (160, 120, 320, 320, 240, 640, LAYOUT_YUYV),
+    (1024, 768, 2048, 1024, 768, 2048, LAYOUT_YUYV),
 ]
 
 

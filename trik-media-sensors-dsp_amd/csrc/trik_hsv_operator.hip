@@ -51,6 +51,9 @@ __constant__ Luts c_luts = make_luts();
 // per-pixel arithmetic (phase1 also yields the clamped colour); with
 // a.meta set (the multi-blob preview) detection is the metapixel flag and no
 // tables are staged.  Every byte of the out_h x out_ll preview is written.
+#ifndef TRIK_PREVIEW_MAP_LDS
+#define TRIK_PREVIEW_MAP_LDS 1
+#endif
 #ifndef TRIK_PREVIEW_Q
 #define TRIK_PREVIEW_Q 2
 #endif
@@ -58,6 +61,7 @@ struct PreviewGeom {
   FastDiv per_frame;  // out_h * quads per row
   FastDiv per_row;    // quads per row
   uint32_t total;
+  uint32_t map_off;  // LDS byte offset of the row and column maps as u16 (0xFFFF = -1), or 0: read from memory
 };
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8)))
 void preview_gather_kernel(PreviewArgs a, PreviewGeom g) {
@@ -69,7 +73,18 @@ void preview_gather_kernel(PreviewArgs a, PreviewGeom g) {
     lds_u128_wptr dst = (lds_u128_wptr)(uintptr_t)0;
     for (int i = threadIdx.x; i < (int)(sizeof(StripeTables) / 16); i += blockDim.x) dst[i] = src[i];
   }
+  typedef __attribute__((address_space(3))) uint16_t* lds_u16_ptr;
+  const lds_u16_ptr maps = (lds_u16_ptr)(uintptr_t)g.map_off;  // [out_h] rows, then [out_w] columns
+  if (g.map_off) {
+    for (int i = threadIdx.x; i < a.out_h; i += blockDim.x) maps[i] = (uint16_t)a.last_row[i];
+    for (int i = threadIdx.x; i < a.out_w; i += blockDim.x) maps[a.out_h + i] = (uint16_t)a.last_col[i];
+  }
   __syncthreads();
+  auto map_at = [&](const int32_t* mem, int off, int i) -> int {
+    if (!g.map_off) return mem[i];
+    const uint32_t v = maps[off + i];
+    return v == 0xFFFFu ? -1 : (int)v;
+  };
   const int t = threadIdx.x;
   const uint32_t hue_lane = (uint32_t)offsetof(StripeTables, hue) + ((t % kHueCopies) << 2);
   const uint32_t m43_lane = (uint32_t)offsetof(StripeTables, m43) + ((t % kM43Copies) << 2);
@@ -97,11 +112,11 @@ void preview_gather_kernel(PreviewArgs a, PreviewGeom g) {
     int sr[kQ], sc[kQ][2];
 #pragma unroll
     for (int u = 0; u < kQ; ++u) {
-      sr[u] = ok[u] ? a.last_row[rr[u]] : -1;
+      sr[u] = ok[u] ? map_at(a.last_row, 0, (int)rr[u]) : -1;
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         const int c = 2 * (int)qq[u] + k;
-        sc[u][k] = ok[u] && c < a.out_w ? a.last_col[c] : -1;
+        sc[u][k] = ok[u] && c < a.out_w ? map_at(a.last_col, a.out_h, c) : -1;
       }
     }
     uint32_t w[kQ][2];  // each pixel as a YUYV word with its Y in byte 0
@@ -358,7 +373,7 @@ static int launch_gather(const PreviewArgs& a, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(preview_gather_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(StripeTables));
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     if (e != hipSuccess) return e;
     attr = true;
   }
@@ -373,9 +388,18 @@ static int launch_gather(const PreviewArgs& a, hipStream_t s) {
   g.per_frame = make_div((uint32_t)(a.out_h * qpr));
   g.per_row = make_div((uint32_t)qpr);
   g.total = (uint32_t)total;
+  // the maps in LDS behind the tables when they fit two workgroups per CU and
+  // every source coordinate fits u16
+  const uint32_t tables_bytes = a.meta ? 16u : (uint32_t)sizeof(StripeTables);
+  const int64_t map_bytes = 2LL * (a.out_w + a.out_h);
+  g.map_off = TRIK_PREVIEW_MAP_LDS && a.width < 65535 && a.height < 65535 &&
+                      tables_bytes + map_bytes <= 80 * 1024
+                  ? tables_bytes
+                  : 0u;
+  const size_t lds = g.map_off ? (size_t)(tables_bytes + map_bytes) : (a.meta ? 0 : sizeof(StripeTables));
   const int64_t blocks = (total + 1024LL * TRIK_PREVIEW_Q - 1) / (1024LL * TRIK_PREVIEW_Q), slots = 2LL * cus;
   hipLaunchKernelGGL(preview_gather_kernel, dim3((unsigned)(blocks < slots ? blocks : slots)), dim3(1024),
-                     a.meta ? 0 : sizeof(StripeTables), s, a, g);
+                     lds, s, a, g);
   return hipGetLastError();
 }
 
