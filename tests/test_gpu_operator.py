@@ -129,8 +129,9 @@ def test_batch_auto_range(hsv, oracle_mod, w, h, ll, layout, kind):
 
 @pytest.mark.parametrize("layout", [LAYOUT_YUYV, LAYOUT_OV7670])
 def test_batch_auto_range_large_batch(hsv, oracle_mod, layout):
-    """>= 512 frames take the two-pass kernel, fewer the one-pass kernel
-    (operator.hip:launch_auto_range): both = the oracle, frame by frame."""
+    """>= 512 frames take the two-pass kernel, fewer the one-pass kernel with
+    256 lanes per frame, <= 32 frames the one with 1024
+    (operator.hip:launch_auto_range): all three = the oracle, frame by frame."""
     import torch
 
     w, h, n = 160, 120, 520
@@ -141,6 +142,8 @@ def test_batch_auto_range_large_batch(hsv, oracle_mod, layout):
     got = hsv.batch_auto_range(dev, w, h, ll, layout).cpu().numpy().astype(np.int64)
     few = hsv.batch_auto_range(dev[:16 * fb], w, h, ll, layout).cpu().numpy().astype(np.int64)
     assert np.array_equal(got[:16], few)
+    mid = hsv.batch_auto_range(dev[:64 * fb], w, h, ll, layout).cpu().numpy().astype(np.int64)
+    assert np.array_equal(got[:64], mid)
     host = dev.cpu().numpy()
     for f in range(n):
         _, want, _ = oracle_mod.run(host[f * fb:(f + 1) * fb], w, h, ll, layout, T0,

@@ -214,6 +214,9 @@ __global__ __launch_bounds__(64) void overlay_kernel(PreviewArgs a, const TrikHs
 }
 
 constexpr int kRangeBlock = 256;
+#ifndef TRIK_RANGE_WIDE_FRAMES
+#define TRIK_RANGE_WIDE_FRAMES 32
+#endif
 
 // H, S, V bytes of one pixel (WSEQ:207-249), branch-free as the hot kernel's
 // phase1 (clamp8_shift6 on v_dot4 presums, the hue case as selects), with
@@ -273,9 +276,9 @@ __device__ __forceinline__ void bin_add(uint32_t* cnt, uint32_t* lst, uint32_t v
 // chip, slower for a single frame (one workgroup, latency-bound).  Either way
 // the winner is, among the values with count M, the one with the earliest
 // last occurrence (see the file comment).
-template <bool kTwoPass>
-__global__ __launch_bounds__(kRangeBlock) void auto_range_kernel(AutoRangeArgs a) {
-  constexpr int kWaves = kRangeBlock / 64;
+template <bool kTwoPass, int kBlock>
+__global__ __launch_bounds__(kBlock) void auto_range_kernel(AutoRangeArgs a) {
+  constexpr int kWaves = kBlock / 64;
   constexpr int kLastSets = kTwoPass ? 1 : kWaves;
   __shared__ uint32_t cnt[kWaves][3][256];
   __shared__ uint32_t lst[kLastSets][3][256];
@@ -304,9 +307,9 @@ __global__ __launch_bounds__(kRangeBlock) void auto_range_kernel(AutoRangeArgs a
   // (row, col) advanced incrementally (no division per pixel)
   auto zone = [&](auto fn) {
     if (zn <= 0) return;
-    const uint32_t zwu = (uint32_t)zw, sq = (uint32_t)kRangeBlock / zwu, sr = (uint32_t)kRangeBlock % zwu;
+    const uint32_t zwu = (uint32_t)zw, sq = (uint32_t)kBlock / zwu, sr = (uint32_t)kBlock % zwu;
     uint32_t zr = (uint32_t)tid / zwu, zc = (uint32_t)tid % zwu;
-    for (uint32_t i = (uint32_t)tid; i < (uint32_t)zn; i += kRangeBlock) {
+    for (uint32_t i = (uint32_t)tid; i < (uint32_t)zn; i += kBlock) {
       fn(r0 + (int)zr, c0 + (int)zc);
       zc += sr;
       zr += sq;
@@ -418,11 +421,15 @@ int launch_preview(const PreviewArgs& a, const TrikHsvTargetSums* sums, int sums
 
 int launch_auto_range(const AutoRangeArgs& a, hipStream_t s) {
   if (a.n_frames <= 0) return hipSuccess;
-  // one workgroup per frame; two passes once the batch fills the chip (2 per CU)
+  // one workgroup per frame; two passes once the batch fills the chip (2 per
+  // CU); a few frames (process() takes one) get 1024 lanes each: the pass over
+  // the zone is a latency-bound chain per lane, 4x shorter
   if (a.n_frames >= 512)
-    hipLaunchKernelGGL(auto_range_kernel<true>, dim3((unsigned)a.n_frames), dim3(kRangeBlock), 0, s, a);
+    hipLaunchKernelGGL((auto_range_kernel<true, kRangeBlock>), dim3((unsigned)a.n_frames), dim3(kRangeBlock), 0, s, a);
+  else if (a.n_frames <= TRIK_RANGE_WIDE_FRAMES)
+    hipLaunchKernelGGL((auto_range_kernel<false, 1024>), dim3((unsigned)a.n_frames), dim3(1024), 0, s, a);
   else
-    hipLaunchKernelGGL(auto_range_kernel<false>, dim3((unsigned)a.n_frames), dim3(kRangeBlock), 0, s, a);
+    hipLaunchKernelGGL((auto_range_kernel<false, kRangeBlock>), dim3((unsigned)a.n_frames), dim3(kRangeBlock), 0, s, a);
   return hipGetLastError();
 }
 
