@@ -129,6 +129,12 @@ void preview_gather_kernel(PreviewArgs a, PreviewGeom g) {
         if (sr[u] < 0 || sc[u][k] < 0) continue;
         if (a.layout == TRIK_HSV_LAYOUT_YUYV && a.aligned4) {
           w[u][k] = *reinterpret_cast<const uint32_t*>(fr + (int64_t)sr[u] * ll + 4 * (sc[u][k] >> 1));
+        } else if (a.layout == TRIK_HSV_LAYOUT_OV7670 && a.aligned4) {
+          // Y from the luma plane, the V, U byte pair as one u16 (OSEQ:343-387)
+          const int64_t off = (int64_t)sr[u] * ll + sc[u][k];
+          const uint32_t Y = fr[off];
+          const uint32_t vu = *reinterpret_cast<const uint16_t*>(fr + ll * a.height + (off & ~(int64_t)1));
+          w[u][k] = Y | ((vu >> 8) << 8) | ((vu & 0xFFu) << 24);
         } else {
           int Y, U, V;
           fetch_yuv(fr, a.height, a.line_length, a.layout, sr[u], sc[u][k], Y, U, V);
