@@ -1,0 +1,157 @@
+// kbench -- development A/B timer for libtrik_hsv.so variants (no torch).
+//
+// Loads each library given on the command line (dlopen, RTLD_LOCAL), fills one
+// device batch with the library's own synthetic-frame generator (first library),
+// and times trik_hsv_batch_sums with HIP events on one stream, interleaving the
+// variants round by round.  Every variant's sums are compared with the first
+// variant's (bit for bit).  Development only: not part of the product or tests.
+//
+// build: hipcc -O2 -std=c++17 --offload-arch=gfx950 -o scripts/kbench scripts/kbench.cpp -ldl
+// usage: kbench [-f frames] [-w W] [-h H] [-t targets] [-k kind] [-n iters] [-r rounds]
+//               [-m hot] [-l layout] lib.so [lib.so ...]
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../include/trik_hsv.h"
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(2);                                                                  \
+    }                                                                           \
+  } while (0)
+
+struct Lib {
+  std::string path;
+  void* so = nullptr;
+  decltype(&TRIK_VIDTRANSCODE_CV_create) create;
+  decltype(&trik_hsv_batch_sums) sums;
+  decltype(&trik_hsv_synth) synth;
+  decltype(&trik_hsv_set_hot_kernel) set_hot;
+  decltype(&trik_hsv_last_error) last_error;
+  decltype(&trik_hsv_chroma_share) share;
+  TRIK_VIDTRANSCODE_CV_Handle h = nullptr;
+  std::vector<float> ms;
+};
+
+template <typename F>
+static void sym(void* so, const char* name, F& f) {
+  f = reinterpret_cast<F>(dlsym(so, name));
+  if (!f) {
+    fprintf(stderr, "missing %s: %s\n", name, dlerror());
+    exit(2);
+  }
+}
+
+int main(int argc, char** argv) {
+  int frames = 4096, W = 640, H = 480, T = 4, kind = 0, iters = 20, rounds = 3, hot = 2, layout = 0;
+  int opt;
+  while ((opt = getopt(argc, argv, "f:w:h:t:k:n:r:m:l:")) != -1) {
+    switch (opt) {
+      case 'f': frames = atoi(optarg); break;
+      case 'w': W = atoi(optarg); break;
+      case 'h': H = atoi(optarg); break;
+      case 't': T = atoi(optarg); break;
+      case 'k': kind = atoi(optarg); break;
+      case 'n': iters = atoi(optarg); break;
+      case 'r': rounds = atoi(optarg); break;
+      case 'm': hot = atoi(optarg); break;
+      case 'l': layout = atoi(optarg); break;
+      default: return 2;
+    }
+  }
+  std::vector<Lib> libs;
+  for (int i = optind; i < argc; ++i) {
+    Lib L;
+    L.path = argv[i];
+    L.so = dlopen(argv[i], RTLD_NOW | RTLD_LOCAL);
+    if (!L.so) {
+      fprintf(stderr, "dlopen %s: %s\n", argv[i], dlerror());
+      return 2;
+    }
+    sym(L.so, "TRIK_VIDTRANSCODE_CV_create", L.create);
+    sym(L.so, "trik_hsv_batch_sums", L.sums);
+    sym(L.so, "trik_hsv_synth", L.synth);
+    sym(L.so, "trik_hsv_set_hot_kernel", L.set_hot);
+    sym(L.so, "trik_hsv_last_error", L.last_error);
+    sym(L.so, "trik_hsv_chroma_share", L.share);
+    libs.push_back(L);
+  }
+  if (libs.empty()) return 2;
+  const TRIK_VIDTRANSCODE_CV_InArgsAlg all[4] = {
+      {0, 30, 50, 100, 30, 100, 0}, {90, 150, 40, 100, 20, 100, 0},
+      {200, 260, 40, 100, 20, 100, 0}, {330, 20, 30, 100, 30, 100, 0}};
+  const int ll = layout == 0 ? 2 * W : W;
+  const int64_t fb = (int64_t)H * ll * (layout == 0 ? 1 : 2);
+  uint8_t* d_frames = nullptr;
+  CK(hipMalloc(&d_frames, fb * frames));
+  TrikHsvTargetSums* d_sums = nullptr;
+  const size_t sb = sizeof(TrikHsvTargetSums) * (size_t)frames * T;
+  CK(hipMalloc(&d_sums, sb));
+  hipStream_t s;
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  TrikHsvFrameBatch b = {d_frames, fb, frames, W, H, ll, layout};
+  if (libs[0].synth(&b, 0, kind, 0x7A1Cull, s)) {
+    fprintf(stderr, "synth: %s\n", libs[0].last_error());
+    return 2;
+  }
+  std::vector<TrikHsvTargetSums> ref(sb / sizeof(TrikHsvTargetSums)), got(ref.size());
+  for (size_t i = 0; i < libs.size(); ++i) {
+    Lib& L = libs[i];
+    if (L.create(nullptr, &L.h)) return 2;
+    L.set_hot(hot);
+    CK(hipMemsetAsync(d_sums, 0, sb, s));
+    if (L.sums(L.h, &b, all, T, d_sums, s)) {
+      fprintf(stderr, "%s: %s\n", L.path.c_str(), L.last_error());
+      return 2;
+    }
+    CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(i ? got.data() : ref.data(), d_sums, sb, hipMemcpyDeviceToHost));
+    if (i && memcmp(got.data(), ref.data(), sb)) {
+      size_t k = 0;
+      while (k < ref.size() && !memcmp(&got[k], &ref[k], sizeof got[k])) ++k;
+      printf("MISMATCH %s vs %s at frame %zu range %zu\n", L.path.c_str(), libs[0].path.c_str(), k / T, k % T);
+    }
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int r = 0; r < rounds; ++r)
+    for (Lib& L : libs) {
+      L.set_hot(hot);
+      for (int w = 0; w < 3; ++w) L.sums(L.h, &b, all, T, d_sums, s);
+      for (int k = 0; k < iters; ++k) {
+        CK(hipEventRecord(e0, s));
+        L.sums(L.h, &b, all, T, d_sums, s);
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        L.ms.push_back(ms);
+      }
+    }
+  const double bytes = (double)fb * frames;
+  for (Lib& L : libs) {
+    std::vector<float> v = L.ms;
+    std::sort(v.begin(), v.end());
+    double mean = 0;
+    for (float x : v) mean += x;
+    mean /= v.size();
+    const double med = v[v.size() / 2];
+    double sh = -1;
+    L.share(L.h, &sh);
+    printf("%-40s T=%d kind=%d share %.4f  median %.4f ms  mean %.4f  min %.4f  frac %.4f\n", L.path.c_str(), T, kind, sh, med,
+           mean, v[0], bytes / (med * 1e-3) / 8e12);
+  }
+  return 0;
+}

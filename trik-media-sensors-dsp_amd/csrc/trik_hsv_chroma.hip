@@ -57,22 +57,28 @@ static_assert(kChunkWords == 4 || kChunkWords == 8, "chunk width");
 constexpr int kMaxSteps = kChunkWords == 8 ? 31 : 63;
 static_assert((kChunkWords == 8 ? 4 : 2) * 2 * kMaxSteps <= 255, "flush group sums fit a byte");
 constexpr int kQFlush = 7;
-constexpr int kQueueCap = 128;  // entries per wave: < 64 waiting + <= 64 added by one word slot
+constexpr int kQueueCap = 128;  // blob kernel, entries per wave: < 64 waiting + <= 64 added by one word slot
+// Hot kernel: at most 15 waves (960 lanes) per workgroup; a wave drains when
+// its queue holds >= kDrainAt entries, checked after every second word slot,
+// so the queue holds < kDrainAt + 128 entries.
+constexpr int kHotLanes = 960;
+constexpr int kDrainAt = 60;
+constexpr int kHotQueueCap = kDrainAt - 1 + 128;
 
 // LDS image of the chroma kernel (dynamic LDS from address 0).  The block
 // masks and the mask-pair table sit below 64 KiB so their reads take an
 // immediate DS offset; the run descriptors follow.
-constexpr uint32_t kLdsBlocks = 0;                    // u8  [4096]  M1 | M2 << 4 of the 16-chroma block
+constexpr uint32_t kLdsBlocks = 0;                    // u16 [4096]  the 16-chroma block's pair offset | cut << 8
 constexpr uint32_t kLdsPairs = 8192;                  // u32 [kChromaPalette][2] byte-spread (M1, M2) of the palette
-constexpr uint32_t kLdsLut43 = 10240;                 // u16 [256]   s_mult43_div (WSEQ:389-407)
+constexpr uint32_t kLdsLut43 = kLdsPairs + 8 * kChromaPalette;  // u16 [256]   s_mult43_div (WSEQ:389-407)
 constexpr uint32_t kLdsLut255 = kLdsLut43 + 512;      // u16 [256]   s_mult255_div
 constexpr uint32_t kLdsHue = kLdsLut255 + 512;        // u8  [256]   hue test per H (bit t = range t)
 constexpr uint32_t kLdsSat = kLdsHue + 256;           // u8  [256]   saturation test per S
 constexpr uint32_t kLdsVal = kLdsSat + 256;           // u8  [256]   value test per V
-constexpr uint32_t kLdsRuns = 12288;                  // u16 [65536] b1 | b2 << 8 per chroma
-constexpr uint32_t kLdsQueues = kLdsRuns + 131072;    // per wave: kQueueCap x {word, pos}
-static_assert(kLdsVal + 256 <= kLdsRuns, "LDS layout");
-constexpr uint32_t kLdsBytes = kLdsQueues + 16 * kQueueCap * 8;
+constexpr uint32_t kLdsRuns = kLdsVal + 256;          // u16 [65536] b1 | b2 << 8 per chroma
+constexpr uint32_t kLdsQueues = kLdsRuns + 131072;    // per wave: kHotQueueCap (blob: kQueueCap) x {word, pos}
+static_assert(kLdsBlocks + 8192 <= kLdsPairs, "LDS layout");
+constexpr uint32_t kLdsBytes = kLdsQueues + (kHotLanes / 64) * kHotQueueCap * 8;
 static_assert(kLdsBytes <= 160 * 1024, "chroma kernel LDS image");
 
 typedef __attribute__((address_space(3))) uint8_t* lds8_t;
@@ -93,27 +99,31 @@ __device__ __forceinline__ void st64(uint32_t a, uint32_t x, uint32_t y) {
 }
 
 // The fast-path masks of the two pixels of YUYV word w under run descriptor
-// d = b1 | b2 << 8 and mask pair (m1, m2): with lt = Y < b1, le = Y <= b2,
-// e = le ? (lt ? m1 : m2) : 0.  Byte operands straight from w and d by SDWA
-// compares; the selects follow all compares (the VALU-writes-SGPR ->
-// v_cndmask distance needs no nops).  q0 / q1 (wave masks, SALU) flag the
-// pixels the exact path resolves: a window pixel (lt and not le, where the
-// select gives 0) or any pixel of an exception-code word (le is cleared, so
-// the select gives 0 as well).  vm masks lanes without a valid row.
-__device__ __forceinline__ void select2(uint32_t w, uint32_t d, uint32_t m1, uint32_t m2, uint64_t vm,
+// d = b1 | b2 << 8, block word bw (cut A in its byte 1) and mask pair (m1, m2): with lt = Y < b1,
+// le = Y <= b2, ge = Y >= A, e = le && ge ? (lt ? m1 : m2) : 0.  Byte operands
+// straight from w and d by SDWA compares; the selects follow all compares (the
+// VALU-writes-SGPR -> v_cndmask distance needs no nops).  q0 / q1 (wave masks,
+// SALU) flag the pixels the exact path resolves: a window pixel (lt and not
+// le, where the select gives 0; windows lie above the cut) or any pixel of an
+// exception-code word (le is cleared, so the select gives 0 as well).  vm
+// masks lanes without a valid row.
+__device__ __forceinline__ void select2(uint32_t w, uint32_t d, uint32_t bw, uint32_t m1, uint32_t m2, uint64_t vm,
                                         uint32_t& e0, uint32_t& e1, uint64_t& q0, uint64_t& q1) {
-  uint64_t x, lt0, lt1, le0, le1;
+  uint64_t x, lt0, lt1, le0, le1, ge0, ge1;
   asm volatile(
       "v_cmp_eq_u32_e64 %[x], %[k], %[d]\n\t"
       "v_cmp_gt_u32_sdwa %[lt0], %[d], %[w] src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"
       "v_cmp_gt_u32_sdwa %[lt1], %[d], %[w] src0_sel:BYTE_0 src1_sel:BYTE_2\n\t"
       "v_cmp_ge_u32_sdwa %[le0], %[d], %[w] src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"
-      "v_cmp_ge_u32_sdwa %[le1], %[d], %[w] src0_sel:BYTE_1 src1_sel:BYTE_2"
-      : [x] "=&s"(x), [lt0] "=&s"(lt0), [lt1] "=&s"(lt1), [le0] "=&s"(le0), [le1] "=&s"(le1)
-      : [w] "v"(w), [d] "v"(d), [k] "s"(kChromaExc));
+      "v_cmp_ge_u32_sdwa %[le1], %[d], %[w] src0_sel:BYTE_1 src1_sel:BYTE_2\n\t"
+      "v_cmp_le_u32_sdwa %[ge0], %[a], %[w] src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"
+      "v_cmp_le_u32_sdwa %[ge1], %[a], %[w] src0_sel:BYTE_1 src1_sel:BYTE_2"
+      : [x] "=&s"(x), [lt0] "=&s"(lt0), [lt1] "=&s"(lt1), [le0] "=&s"(le0), [le1] "=&s"(le1), [ge0] "=&s"(ge0),
+        [ge1] "=&s"(ge1)
+      : [w] "v"(w), [d] "v"(d), [a] "v"(bw), [k] "s"(kChromaExc));
   q0 = (x | (lt0 & ~le0)) & vm;
   q1 = (x | (lt1 & ~le1)) & vm;
-  const uint64_t k0 = le0 & ~x & vm, k1 = le1 & ~x & vm;
+  const uint64_t k0 = le0 & ge0 & ~x & vm, k1 = le1 & ge1 & ~x & vm;
   asm volatile(
       "v_cndmask_b32_e64 %[e0], %[m2], %[m1], %[lt0]\n\t"
       "v_cndmask_b32_e64 %[e1], %[m2], %[m1], %[lt1]\n\t"
@@ -163,17 +173,20 @@ __global__ __launch_bounds__(256) void chroma_summary_kernel(const RangeTables* 
   }
   // runs up to and including the last nonzero one
   const int n = last_nz_run + 1;  // 0: all zero
-  uint32_t s;
-  if (n == 0) s = 0;
-  else {
-    // a: end of the first run (its value v1 = the mask at Y = 0, maybe 0);
-    // ab: end of run 2 (n == 2) or of the last nonzero run (n > 2)
-    const int a = ends[0];
-    const int ab = n == 1 ? a : last_nz_end;
-    s = (uint32_t)(n > 2 ? 3 : n) | (vals[0] << 4) | ((n == 2 ? vals[1] : 0u) << 8) | ((uint32_t)a << 12) |
-        ((uint32_t)ab << 21);
-  }
-  ct->summary[c] = s;
+  // a: end of the first run (its value v1 = the mask at Y = 0, maybe 0);
+  // ab: end of run 2 (n == 2) or of the last nonzero run (n > 2)
+  auto pack = [&](int nn, uint32_t v1, uint32_t v2, int a) -> uint32_t {
+    if (nn == 0) return 0u;
+    const int ab = nn == 1 ? a : last_nz_end;
+    return (uint32_t)(nn > 2 ? 3 : nn) | (v1 << 4) | ((nn == 2 ? v2 : 0u) << 8) | ((uint32_t)a << 12) |
+           ((uint32_t)ab << 21);
+  };
+  ct->summary[c] = pack(n, vals[0], vals[1], ends[0]);
+  // the profile from its first nonzero Y on: without a leading zero run the
+  // same; with one, the runs after it (runs 1 and 2 become runs 0 and 1)
+  const bool lead0 = vals[0] == 0u && n > 0;
+  ct->summary_drop[c] = lead0 ? pack(n - 1, vals[1], vals[2], ends[1]) : ct->summary[c];
+  ct->first_nz[c] = (uint16_t)(n == 0 ? 256 : (lead0 ? ends[0] : 0));
 }
 
 // The run descriptor of one chroma under block masks (M1, M2).  With
@@ -213,51 +226,74 @@ __device__ __forceinline__ uint32_t chroma_cost(uint32_t d) {
   return L * (512u - L);
 }
 
-// One thread per 16-chroma block (U >> 4, V): the mask pair with the fewest
-// expected exact-path words over its chromas (ties: the smallest
-// k = M1 | M2 << 4).  PALETTE = false: the unrestricted choice, counted in
-// pair_hist.  PALETTE = true: the choice among the palette's pairs (the
-// unrestricted one when it made the palette, which is nearly always), then
-// the block byte (the pair's palette offset) and the run descriptors under it.
+// The descriptor of chroma i of a block under mask pair k and cut A: its
+// profile is zero below first_nz = f, so with f > A the cut changes nothing
+// (the full summary), with f == A the profile from A on is described (the
+// summary without the leading zero run), and with f < A the cut would clear
+// nonzero pixels: the exception code.
+__device__ __forceinline__ uint32_t chroma_desc_cut(uint32_t sf, uint32_t sd, uint32_t f, uint32_t k, uint32_t A) {
+  if (f < A) return kChromaExc;
+  return chroma_desc(f == A ? sd : sf, k & 15u, k >> 4);
+}
+
+// One workgroup per 16-chroma block b = (V << 4) | (U >> 4), one thread per
+// mask pair k = M1 | M2 << 4: each thread finds the cut A (0, or the first
+// nonzero Y of one of the block's chromas) with the fewest expected
+// exact-path words over the block, and the workgroup keeps the cheapest
+// (cost, k, A) (ties: smaller k, then smaller A).  PALETTE = false: all pairs
+// whose masks occur in the block; the choice is counted in pair_hist.
+// PALETTE = true: the palette's pairs only (the same choice when the
+// unrestricted pair made the palette, which is nearly always); then the block
+// byte (the pair's palette offset), the cut and the run descriptors.
 template <bool PALETTE>
 __global__ __launch_bounds__(256) void chroma_block_kernel(ChromaTables* ct) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;  // (V << 4) | (U >> 4)
-  if (b >= 4096) return;
+  __shared__ uint32_t sf[16], sd[16], fz[16];
+  __shared__ unsigned long long best;
+  const int b = blockIdx.x;
+  const uint32_t k = threadIdx.x;
   const uint32_t c0 = ((uint32_t)(b >> 4) << 8) | ((uint32_t)(b & 15) << 4);
-  uint32_t s[16];
+  if (k < 16) {
+    sf[k] = ct->summary[c0 + k];
+    sd[k] = ct->summary_drop[c0 + k];
+    fz[k] = ct->first_nz[c0 + k];
+  }
+  if (k == 0) best = ~0ull;
+  __syncthreads();
   uint32_t present = 1u;  // mask values appearing (value 0 always a candidate)
-#pragma unroll
   for (int i = 0; i < 16; ++i) {
-    s[i] = ct->summary[c0 + i];
-    if (s[i] & 3u) present |= 1u << ((s[i] >> 4) & 15u);
-    if ((s[i] & 3u) == 2u) present |= 1u << ((s[i] >> 8) & 15u);
+    if (sf[i] & 3u) present |= 1u << ((sf[i] >> 4) & 15u);
+    if ((sf[i] & 3u) == 2u) present |= 1u << ((sf[i] >> 8) & 15u);
+    if (sd[i] & 3u) present |= 1u << ((sd[i] >> 4) & 15u);
+    if ((sd[i] & 3u) == 2u) present |= 1u << ((sd[i] >> 8) & 15u);
   }
-  auto block_cost = [&](uint32_t k) {
-    uint32_t cost = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) cost += chroma_cost(chroma_desc(s[i], k & 15u, k >> 4));
-    return cost;
-  };
-  uint32_t best = 0xFFFFFFFFu, best_k = 0;
-  if (!PALETTE || ct->palette_of[ct->blocks[b]] == 0xFFu) {
-    for (uint32_t k = 0; k < 256; ++k) {
-      if (PALETTE ? ct->palette_of[k] == 0xFFu : (!((present >> (k & 15u)) & 1u) || !((present >> (k >> 4)) & 1u)))
-        continue;
-      const uint32_t cost = block_cost(k);
-      if (cost < best) { best = cost; best_k = k; }
+  const bool skip = PALETTE ? ct->palette_of[k] == 0xFFu
+                            : (!((present >> (k & 15u)) & 1u) || !((present >> (k >> 4)) & 1u));
+  if (!skip) {
+    unsigned long long mine = ~0ull;
+    for (int j = -1; j < 16; ++j) {
+      const uint32_t A = j < 0 ? 0u : fz[j];
+      if (j >= 0 && (A == 0u || A > 255u)) continue;
+      uint32_t cost = 0;
+      for (int i = 0; i < 16; ++i) cost += chroma_cost(chroma_desc_cut(sf[i], sd[i], fz[i], k, A));
+      const unsigned long long key = ((unsigned long long)cost << 17) | ((unsigned long long)k << 9) | A;
+      if (key < mine) mine = key;
     }
-  } else {
-    best_k = ct->blocks[b];
+    atomicMin(&best, mine);
   }
+  __syncthreads();
+  const uint32_t bk = (uint32_t)(best >> 9) & 255u, bA = (uint32_t)best & 511u;
   if (!PALETTE) {
-    ct->blocks[b] = (uint8_t)best_k;
-    atomicAdd(&ct->pair_hist[best_k], 1u);
+    if (k == 0) {
+      ct->best[b] = best;
+      atomicAdd(&ct->pair_hist[bk], 1u);
+    }
     return;
   }
-  ct->blocks[b] = ct->palette_of[best_k];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) ct->runs[c0 + i] = (uint16_t)chroma_desc(s[i], best_k & 15u, best_k >> 4);
-  atomicAdd(&ct->flagged_cost, (unsigned long long)block_cost(best_k));
+  if (k < 16) ct->runs[c0 + k] = (uint16_t)chroma_desc_cut(sf[k], sd[k], fz[k], bk, bA);
+  if (k == 0) {
+    ct->blocks[b] = (uint16_t)(ct->palette_of[bk] | (bA << 8));
+    atomicAdd(&ct->flagged_cost, best >> 17);
+  }
 }
 
 // One workgroup of 256: the palette is the (up to) kChromaPalette most used
@@ -375,7 +411,7 @@ template <int LAYOUT, int NR, bool MASKS, int CW>
 __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaGeom g, const ChromaTables* ct) {
   const int t = threadIdx.x;
   {  // stage block masks, the mask-pair table and the run descriptors
-    for (int i = t; i < 4096 / 16; i += blockDim.x)
+    for (int i = t; i < 8192 / 16; i += blockDim.x)
       *(lds128_t)(uintptr_t)(kLdsBlocks + 16 * i) = reinterpret_cast<const u32x4*>(ct->blocks)[i];
     for (int i = t; i < kChromaPalette; i += blockDim.x) st64(kLdsPairs + 8 * i, ct->palette[2 * i], ct->palette[2 * i + 1]);
     for (int i = t; i < 131072 / 16; i += blockDim.x)
@@ -391,8 +427,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
   __syncthreads();
 
   const int lane = t & 63;
-  const uint32_t qbase = kLdsQueues + (uint32_t)(t >> 6) * (kQueueCap * 8);
-  const uint32_t qbase_s = __builtin_amdgcn_readfirstlane(qbase);  // wave-uniform (SGPR)
+  const uint32_t qbase_s = __builtin_amdgcn_readfirstlane(kLdsQueues + (uint32_t)(t >> 6) * (kHotQueueCap * 8));
   const bool active = t < g.k * g.cpr;
   const int col = active ? t % g.cpr : 0;
   const int ro = active ? t / g.cpr : 0;
@@ -438,11 +473,11 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
       ex.EN = ex.SX02 = ex.SX13 = ex.SY02 = ex.SY13 = 0;
       ex.rounds = 0;
     };
-    // One drain round: lanes 0..take-1 resolve queue entries 0..take-1 (two
-    // pixels each) exactly; the rest of the queue moves to the front.
+    // One drain round: lanes 0..take-1 resolve the last take queue entries
+    // (two pixels each) exactly.
     auto drain = [&](int take) {
       if (lane < take) {
-        const u32x2 ent = ld64(qbase + 8u * (uint32_t)lane);
+        const u32x2 ent = ld64(qbase_s + 8u * (uint32_t)(qn - take + lane));
         const uint32_t w = ent.x, x = ent.y & 0xFFFFu, yr = ent.y >> 16;
         // which of the word's pixels the fast path left to this path (select2)
         const uint32_t d = ld16(kLdsRuns + 2u * chroma_of(w));
@@ -465,14 +500,8 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         ex.SY13 += (b0 + b1) * yr;
       }
       if (++ex.rounds == g.flush_rounds) unpack_exc();
-      const int rest = qn - take;
-      if (rest > 0) {
-        u32x2 mv = {0u, 0u};
-        if (lane < rest) mv = ld64(qbase + 8u * (uint32_t)(take + lane));
-        __builtin_amdgcn_wave_barrier();
-        if (lane < rest) st64(qbase + 8u * (uint32_t)lane, mv.x, mv.y);
-      }
-      qn = rest;
+      __builtin_amdgcn_wave_barrier();  // the entries are read before the slots are reused
+      qn -= take;
     };
 
     const uint8_t* pf = active ? p : a.frames + (int64_t)f * a.frame_stride;
@@ -489,7 +518,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         // lanes with a valid row (rows past the frame re-read a valid row:
         // their pixels are masked out of the sums and the queue)
         const uint64_t vm = FULL ? ~0ull : __builtin_amdgcn_ballot_w64(valid);
-        uint32_t c[CW], ba[CW], d[CW], e[2 * CW];
+        uint32_t c[CW], d[CW], cut[CW], e[2 * CW];
         u32x2 mm[CW];
 #pragma unroll
         for (int i = 0; i < CW; ++i) c[i] = chroma_of(cw[i]);
@@ -497,24 +526,25 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         for (int i = 0; i < CW; ++i) {
 #ifdef TRIK_AB_NO_LDS  // timing attribution only
           d[i] = (c[i] * 0x9E37u) & 0xFFFFu;
-          ba[i] = kLdsPairs + 8u * (c[i] >> 12);
+          cut[i] = 8u * (c[i] >> 12);
 #else
           d[i] = ld16(kLdsRuns + 2u * c[i]);
-          ba[i] = kLdsPairs + ld8(kLdsBlocks + (c[i] >> 4));  // the block byte is the pair's offset
+          // the block word: the pair's palette offset | the cut << 8
+          cut[i] = ld16(kLdsBlocks + ((c[i] >> 3) & 0x1FFEu));
 #endif
         }
 #ifdef TRIK_AB_NO_LDS
 #pragma unroll
-        for (int i = 0; i < CW; ++i) { mm[i].x = ba[i] & 0x01010101u; mm[i].y = (ba[i] >> 1) & 0x01010101u; }
+        for (int i = 0; i < CW; ++i) { mm[i].x = cut[i] & 0x01010101u; mm[i].y = (cut[i] >> 1) & 0x01010101u; }
 #else
 #pragma unroll
-        for (int i = 0; i < CW; ++i) mm[i] = ld64(ba[i]);
+        for (int i = 0; i < CW; ++i) mm[i] = ld64(kLdsPairs + (cut[i] & 0xFFu));
 #endif
         // pin the descriptors as 32-bit values here (ds_read_u16 zero-extends):
         // otherwise the zero extension is sunk past the drain branches and
         // costs a v_and per word
 #pragma unroll
-        for (int i = 0; i < CW; ++i) asm volatile("" : "+v"(d[i]));
+        for (int i = 0; i < CW; ++i) asm volatile("" : "+v"(d[i]), "+v"(cut[i]));
         // per word: the selects, then the words with a pixel for the exact
         // path (a wave mask in SGPRs) are queued
         const uint32_t pos_s = x0 | ((uint32_t)(ro + s * g.k) << 16);
@@ -526,7 +556,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
           e[2 * i + 1] = (cw[i] >> 1) & 0x01010101u;
           q0 = q1 = 0;
 #else
-          select2(cw[i], d[i], mm[i].x, mm[i].y, vm, e[2 * i], e[2 * i + 1], q0, q1);
+          select2(cw[i], d[i], cut[i], mm[i].x, mm[i].y, vm, e[2 * i], e[2 * i + 1], q0, q1);
 #endif
           const uint64_t bal = q0 | q1;
           if (MASKS && valid) {  // verification mode: the exact path writes the flagged pixels
@@ -549,9 +579,10 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
           }
           qn += __builtin_popcountll(bal);
 #ifdef TRIK_AB_NO_DRAIN  // timing attribution only (drops the exception words)
-          if (qn >= 64) qn = 0;
+          if ((i & 1) && qn >= kDrainAt) qn = 0;
 #else
-          if (qn >= 64) drain(64);
+          if (i & 1)
+            while (qn >= kDrainAt) drain(qn < 64 ? qn : 64);
 #endif
 #endif
         }
@@ -632,7 +663,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     };
     if (full) run(std::true_type{});
     else run(std::false_type{});
-    if (qn > 0) drain(qn);
+    while (qn > 0) drain(qn < 64 ? qn : 64);
     unpack_exc();
     Qa += Ba;
     Qb += Bb;
@@ -690,7 +721,7 @@ __global__ __launch_bounds__(kMaxBlock) void blob_chroma_meta_kernel(BlobArgs a,
                                                                       const RangeTables* rt) {
   const int t = threadIdx.x;
   {  // the chroma kernel's tables (one range), zeroed count words
-    for (int i = t; i < 4096 / 16; i += blockDim.x)
+    for (int i = t; i < 8192 / 16; i += blockDim.x)
       *(lds128_t)(uintptr_t)(kLdsBlocks + 16 * i) = reinterpret_cast<const u32x4*>(ct->blocks)[i];
     for (int i = t; i < kChromaPalette; i += blockDim.x) st64(kLdsPairs + 8 * i, ct->palette[2 * i], ct->palette[2 * i + 1]);
     for (int i = t; i < 131072 / 16; i += blockDim.x)
@@ -751,7 +782,7 @@ __global__ __launch_bounds__(kMaxBlock) void blob_chroma_meta_kernel(BlobArgs a,
       const uint4 vy = *reinterpret_cast<const uint4*>(p + r * ll);
       const uint4 vc = *reinterpret_cast<const uint4*>(p + r * ll + plane);
       const uint32_t yy[4] = {vy.x, vy.y, vy.z, vy.w}, cc[4] = {vc.x, vc.y, vc.z, vc.w};
-      uint32_t w[8], d[8], ba[8];
+      uint32_t w[8], d[8], cut[8];
       u32x2 mm[8];
 #pragma unroll
       for (int k = 0; k < 4; ++k) stripe_px::ov7670_words(yy[k], cc[k], w[2 * k], w[2 * k + 1]);
@@ -759,17 +790,17 @@ __global__ __launch_bounds__(kMaxBlock) void blob_chroma_meta_kernel(BlobArgs a,
       for (int i = 0; i < 8; ++i) {
         const uint32_t c = chroma_of(w[i]);
         d[i] = ld16(kLdsRuns + 2u * c);
-        ba[i] = kLdsPairs + ld8(kLdsBlocks + (c >> 4));
+        cut[i] = ld16(kLdsBlocks + ((c >> 3) & 0x1FFEu));
       }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) mm[i] = ld64(ba[i]);
+      for (int i = 0; i < 8; ++i) mm[i] = ld64(kLdsPairs + (cut[i] & 0xFFu));
 #pragma unroll
-      for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(d[i]));
+      for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(d[i]), "+v"(cut[i]));
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         uint32_t e0, e1;
         uint64_t q0, q1;
-        select2(w[i], d[i], mm[i].x, mm[i].y, vm, e0, e1, q0, q1);
+        select2(w[i], d[i], cut[i], mm[i].x, mm[i].y, vm, e0, e1, q0, q1);
         cnt[i >> 1] += e0 + e1;  // one range: the spread masks are 0 or 1
         const uint64_t bal = q0 | q1;
         const uint32_t idx =
@@ -843,24 +874,24 @@ int build_chroma_tables(const RangeTables* t, ChromaTables* ct, hipStream_t s) {
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(&ct->flagged_cost, 0, sizeof(ct->flagged_cost), s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(chroma_block_kernel<false>, dim3(4096 / 256), dim3(256), 0, s, ct);
+  hipLaunchKernelGGL(chroma_block_kernel<false>, dim3(4096), dim3(256), 0, s, ct);
   hipLaunchKernelGGL(chroma_palette_kernel, dim3(1), dim3(256), 0, s, ct);
-  hipLaunchKernelGGL(chroma_block_kernel<true>, dim3(4096 / 256), dim3(256), 0, s, ct);
+  hipLaunchKernelGGL(chroma_block_kernel<true>, dim3(4096), dim3(256), 0, s, ct);
   return hipGetLastError();
 }
 
 // Column chunks of 2*kChunkWords pixels; k rows per step, as many as fit a
-// 1024-lane workgroup, rounded down to whole waves when that keeps >= 7/8 of
+// kHotLanes-lane workgroup, rounded down to whole waves when that keeps >= 7/8 of
 // the lanes (the kernel's uniform fast path needs whole waves).
 bool chroma_geometry(const KernelArgs& a, ChromaGeom& g) {
   const int px = 2 * kChunkWords;
   if (a.width <= 0 || a.width % px || a.height <= 0) return false;
   const int cpr = a.width / px;
-  if (cpr > kMaxBlock) return false;
+  if (cpr > kHotLanes) return false;
   const int64_t need = 16;  // vector loads
   if ((reinterpret_cast<uintptr_t>(a.frames) % need) || (a.frame_stride % need) || (a.line_length % need))
     return false;
-  int k = kMaxBlock / cpr;
+  int k = kHotLanes / cpr;
   for (int kk = k; kk * 8 >= k * 7; --kk)
     if ((kk * cpr) % 64 == 0) { k = kk; break; }
   g.cpr = cpr;

@@ -61,21 +61,32 @@ static_assert(2 * sizeof(StripeTables) <= 160 * 1024, "two workgroups per CU");
 // Tables of the chroma-run kernel (trik_hsv_chroma.hip), one set per group of
 // <= 4 ranges, built on the device from RangeTables:
 //   runs[c]     : descriptor b1 | b2 << 8 of chroma c = U | V << 8: the
-//                 fast path's mask is Y <= b2 ? (Y < b1 ? M1 : M2) : 0; with
-//                 b1 > b2 + 1 the pixels b2 < Y < b1 go to the exact path
-//                 (a "window"), and kChromaExc sends both pixels there
+//                 fast path's mask is Y >= A && Y <= b2 ? (Y < b1 ? M1 : M2) : 0
+//                 (A: the block's cut); with b1 > b2 + 1 the pixels
+//                 b2 < Y < b1 go to the exact path (a "window", always above
+//                 A), and kChromaExc sends both pixels there
 //   summary[c]  : builder scratch (run summary of the chroma's profile)
 constexpr uint32_t kChromaExc = 0x00FFu;  // b1 = 255, b2 = 0: the builder never makes this window
-//   blocks[b]   : final: 8 x the palette slot of block b's mask pair (the
-//                 hot kernel's LDS offset of the pair); builder scratch: the
-//                 pair k = M1 | M2 << 4 itself
+//   blocks[b]   : low byte: 8 x the palette slot of block b's mask pair (the
+//                 hot kernel's LDS offset of the pair); high byte: the block's
+//                 leading-zero cut A: pixels with Y < A are 0 (the
+//                 fast path masks them), so a chroma whose profile is zero
+//                 below A describes only its profile from A on -- the
+//                 0 | M1 | M2 | 0 profiles of overlapping ranges become runs
 //   palette     : the byte-spread (M1, M2) of each palette slot; palette_of[k]
 //                 is 8 x the slot of pair k, or 0xFF; pair_hist: blocks per pair
+//   summary / summary_drop / first_nz : builder scratch, per chroma: the run
+//                 summary of the profile from Y = 0 and from its first nonzero
+//                 Y on, and that Y (256: all zero); best[b]: the block's
+//                 packed (cost, pair, cut) choice
 constexpr int kChromaPalette = 32;  // 8 x slot fits the block byte
 struct alignas(16) ChromaTables {
   uint16_t runs[65536];
-  uint8_t blocks[4096];
+  uint16_t blocks[4096];
   uint32_t summary[65536];
+  uint32_t summary_drop[65536];
+  uint16_t first_nz[65536];
+  unsigned long long best[4096];
   uint32_t pair_hist[256];
   uint32_t palette[2 * kChromaPalette];
   uint8_t palette_of[256];
