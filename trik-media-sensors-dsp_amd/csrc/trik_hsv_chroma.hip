@@ -45,8 +45,8 @@ namespace trik_hsv {
 namespace {
 
 constexpr int kMaxBlock = 1024;
-#ifndef TRIK_CHROMA_PF
-#define TRIK_CHROMA_PF 1  // rows prefetched ahead of the one being processed
+#ifndef TRIK_CHROMA_NT
+#define TRIK_CHROMA_NT 1  // YUYV frame loads with the nontemporal hint
 #endif
 #ifndef TRIK_CHROMA_CW
 #define TRIK_CHROMA_CW 8
@@ -318,8 +318,13 @@ __global__ __launch_bounds__(256) void chroma_palette_kernel(ChromaTables* ct) {
 // ---------------------------------------------------------------------------
 // Hot kernel
 // ---------------------------------------------------------------------------
+// cpr chunk columns per row, k lanes' rows per step (a lane's first piece),
+// rstep rows per step, steps per tile.  YUYV: a lane's chunk is two 16-byte
+// pieces, the second dy rows below and dx pixels right of the first (dy = k,
+// dx = 0, rstep = 2k; rows wider than kHotLanes pieces: dy = 0, dx = W/2,
+// rstep = k); ov7670: one 16-pixel piece (dy = dx = 0, rstep = k).
 struct ChromaGeom {
-  int32_t cpr, k, steps, tiles_per_frame;
+  int32_t cpr, k, rstep, dy, dx, steps, tiles_per_frame;
   int64_t n_tiles;
   int32_t flush_rounds;  // drain rounds between unpacks of the 16-bit exception sums
 };
@@ -340,16 +345,23 @@ __device__ __forceinline__ void wave_sums(uint32_t (&v)[N]) {
   for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x143, 0xC, 0xF, false);
 }
 
-// One chunk = CW YUYV words (2*CW pixels) of a row: CW*4 bytes packed, or
-// 2*CW luma + 2*CW chroma bytes of the ov7670 planes.
+// One chunk = CW YUYV words (2*CW pixels): YUYV, two 16-byte pieces (8
+// pixels each) at p and pb -- the same columns of two rows, so that one load
+// instruction of a wave reads 1 KiB contiguous; ov7670, 2*CW luma + 2*CW
+// chroma bytes of one row of the two planes (pb unused).
 template <int LAYOUT, int CW>
-__device__ __forceinline__ void load_chunk(const uint8_t* p, int64_t plane, uint32_t (&w)[CW]) {
+__device__ __forceinline__ void load_chunk(const uint8_t* p, const uint8_t* pb, int64_t plane,
+                                           uint32_t (&w)[CW]) {
   if (LAYOUT == TRIK_HSV_LAYOUT_YUYV) {
-#pragma unroll
-    for (int j = 0; j < CW / 4; ++j) {
-      const uint4 v = reinterpret_cast<const uint4*>(p)[j];
-      w[4 * j + 0] = v.x; w[4 * j + 1] = v.y; w[4 * j + 2] = v.z; w[4 * j + 3] = v.w;
-    }
+    static_assert(CW == 8, "YUYV chunks are two 16-byte pieces");
+#if TRIK_CHROMA_NT
+    const u32x4 va = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    const u32x4 vb = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pb));
+#else
+    const uint4 va = *reinterpret_cast<const uint4*>(p), vb = *reinterpret_cast<const uint4*>(pb);
+#endif
+    w[0] = va.x; w[1] = va.y; w[2] = va.z; w[3] = va.w;
+    w[4] = vb.x; w[5] = vb.y; w[6] = vb.z; w[7] = vb.w;
   } else {
     uint32_t yy[CW / 2], cc[CW / 2];
     if (CW == 8) {
@@ -431,21 +443,28 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
   const bool active = t < g.k * g.cpr;
   const int col = active ? t % g.cpr : 0;
   const int ro = active ? t / g.cpr : 0;
+  // YUYV: a lane's 8 words are 4 from row y and 4 from row y + k (word i at
+  // x0 + 2 (i & 3)); ov7670: 8 words of row y (word i at x0 + 2i)
+  constexpr bool SPLIT = LAYOUT == TRIK_HSV_LAYOUT_YUYV;
   const int64_t plane = (int64_t)a.height * a.line_length;
-  const int64_t rowstep = (int64_t)g.k * a.line_length;
+  const int64_t rowstep = (int64_t)g.rstep * a.line_length;
+  const int half = SPLIT ? g.dy : 0;  // rows between a chunk's two pieces
+  const uint32_t dx = SPLIT ? (uint32_t)g.dx : 0u;  // and pixels
+  const int64_t hb = (int64_t)half * a.line_length + 2 * (int64_t)dx;
   constexpr int kQBlock = CW == 8 ? 5 : kQFlush;  // Q block: CW * n * (n + 1) <= 255
-  const int col_bytes = LAYOUT == TRIK_HSV_LAYOUT_YUYV ? col * 4 * CW : col * 2 * CW;
-  const uint32_t x0 = (uint32_t)col * 2 * CW;
+  const int col_bytes = LAYOUT == TRIK_HSV_LAYOUT_YUYV ? col * 16 : col * 2 * CW;
+  const uint32_t x0 = (uint32_t)col * (SPLIT ? 8u : 2u * CW);
   const uint32_t voff = (uint32_t)ro * (uint32_t)a.line_length + (uint32_t)col_bytes;
+  auto xoff = [dx](int i) { return SPLIT ? (i < 4 ? 0u : dx) + 2u * (uint32_t)(i & 3) : 2u * (uint32_t)i; };
 
   const int64_t t_begin = g.n_tiles * blockIdx.x / gridDim.x;
   const int64_t t_end = g.n_tiles * (blockIdx.x + 1) / gridDim.x;
   for (int64_t tile = t_begin; tile < t_end; ++tile) {
     const int f = (int)(tile / g.tiles_per_frame);
-    const int r0 = (int)(tile - (int64_t)f * g.tiles_per_frame) * g.k * g.steps;
+    const int r0 = (int)(tile - (int64_t)f * g.tiles_per_frame) * g.rstep * g.steps;
     const int y0 = r0 + ro;
     // wave-uniform (the division runs on the VALU): keeps the step loop scalar
-    const int steps = __builtin_amdgcn_readfirstlane(min(g.steps, (a.height - r0 + g.k - 1) / g.k));
+    const int steps = __builtin_amdgcn_readfirstlane(min(g.steps, (a.height - r0 + g.rstep - 1) / g.rstep));
     const uint8_t* p = a.frames + (int64_t)f * a.frame_stride + (int64_t)y0 * a.line_length + col_bytes;
 
     uint32_t P[CW], O = 0, Q = 0, CumS = 0, CumA = 0, CumB = 0;
@@ -504,9 +523,12 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
       qn -= take;
     };
 
-    const uint8_t* pf = active ? p : a.frames + (int64_t)f * a.frame_stride;
-    const int vsteps = active ? min(steps, (a.height - y0 + g.k - 1) / g.k) : 0;
-    const bool full = (r0 + steps * g.k <= a.height) && (g.k * g.cpr) % 64 == 0;
+    // a row inside the frame for lanes whose rows run past it (re-read, masked)
+    const uint8_t* pf = active && y0 < a.height ? p : a.frames + (int64_t)f * a.frame_stride + col_bytes;
+    // steps whose first (second) piece row lies inside the frame
+    const int vsteps = active ? max(0, min(steps, (a.height - y0 + g.rstep - 1) / g.rstep)) : 0;
+    const int vstepsb = active ? max(0, min(steps, (a.height - y0 - half + g.rstep - 1) / g.rstep)) : 0;
+    const bool full = (r0 + steps * g.rstep <= a.height) && (g.k * g.cpr) % 64 == 0;
     const uint8_t* tbase = a.frames + (int64_t)f * a.frame_stride + (int64_t)r0 * a.line_length;
     auto run = [&](auto full_c) {
       constexpr bool FULL = decltype(full_c)::value;
@@ -514,10 +536,11 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
       // any queue write (the queue shares LDS, so the compiler keeps the
       // order), then the selects, then the exception words are queued.
       auto step = [&](const uint32_t (&cw)[CW], int s) {
-        const bool valid = FULL || s < vsteps;
+        const bool valid = FULL || s < vsteps, validb = SPLIT ? (FULL || s < vstepsb) : valid;
         // lanes with a valid row (rows past the frame re-read a valid row:
         // their pixels are masked out of the sums and the queue)
-        const uint64_t vm = FULL ? ~0ull : __builtin_amdgcn_ballot_w64(valid);
+        const uint64_t vma = FULL ? ~0ull : __builtin_amdgcn_ballot_w64(valid);
+        const uint64_t vmb = FULL ? ~0ull : (SPLIT ? __builtin_amdgcn_ballot_w64(validb) : vma);
         uint32_t c[CW], d[CW], cut[CW], e[2 * CW];
         u32x2 mm[CW];
 #pragma unroll
@@ -547,7 +570,8 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         for (int i = 0; i < CW; ++i) asm volatile("" : "+v"(d[i]), "+v"(cut[i]));
         // per word: the selects, then the words with a pixel for the exact
         // path (a wave mask in SGPRs) are queued
-        const uint32_t pos_s = x0 | ((uint32_t)(ro + s * g.k) << 16);
+        const uint32_t pos_s = x0 | ((uint32_t)(ro + s * g.rstep) << 16);
+        const uint32_t pos_b = pos_s + ((uint32_t)half << 16);
 #pragma unroll
         for (int i = 0; i < CW; ++i) {
           uint64_t q0, q1;
@@ -556,12 +580,12 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
           e[2 * i + 1] = (cw[i] >> 1) & 0x01010101u;
           q0 = q1 = 0;
 #else
-          select2(cw[i], d[i], cut[i], mm[i].x, mm[i].y, vm, e[2 * i], e[2 * i + 1], q0, q1);
+          select2(cw[i], d[i], cut[i], mm[i].x, mm[i].y, i < 4 ? vma : vmb, e[2 * i], e[2 * i + 1], q0, q1);
 #endif
           const uint64_t bal = q0 | q1;
-          if (MASKS && valid) {  // verification mode: the exact path writes the flagged pixels
-            const int y = y0 + s * g.k;
-            uint8_t* mp = a.masks + ((int64_t)f * a.height + y) * a.width + x0 + 2 * i;
+          if (MASKS && (i < 4 ? valid : validb)) {  // verification mode: the exact path writes the flagged pixels
+            const int y = y0 + s * g.rstep + (i < 4 ? 0 : half);
+            uint8_t* mp = a.masks + ((int64_t)f * a.height + y) * a.width + x0 + xoff(i);
             const uint8_t m0 = (uint8_t)(pack_bits(e[2 * i]) << a.mask_shift);
             const uint8_t m1 = (uint8_t)(pack_bits(e[2 * i + 1]) << a.mask_shift);
             if (!__builtin_amdgcn_inverse_ballot_w64(q0)) mp[0] = a.mask_shift ? (uint8_t)(mp[0] | m0) : m0;
@@ -575,7 +599,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
           if (__builtin_amdgcn_inverse_ballot_w64(bal)) {
             const uint32_t qa = __builtin_amdgcn_readfirstlane(qbase_s + 8u * (uint32_t)qn) + 8u * idx;
             *(lds32_t)(uintptr_t)qa = cw[i];
-            *(lds32_t)(uintptr_t)(qa + 4u) = pos_s + 2u * (uint32_t)i;
+            *(lds32_t)(uintptr_t)(qa + 4u) = (i < 4 ? pos_s : pos_b) + xoff(i);
           }
           qn += __builtin_popcountll(bal);
 #ifdef TRIK_AB_NO_DRAIN  // timing attribution only (drops the exception words)
@@ -622,44 +646,27 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
           nb = 0;
         }
       };
-#if TRIK_CHROMA_PF == 2
-      // rows prefetched two steps ahead (three buffers, unrolled by 3); loads
-      // past the tile's last step re-read its last row
-      auto row_ptr = [&](int s) -> const uint8_t* {
-        if (FULL) return tbase + (int64_t)(s < steps ? s : steps - 1) * rowstep + voff;
-        return s < vsteps ? pf + (int64_t)s * rowstep : pf;
-      };
-      uint32_t wa[CW], wb[CW], wc[CW];
-      load_chunk<LAYOUT, CW>(row_ptr(0), plane, wa);
-      load_chunk<LAYOUT, CW>(row_ptr(1), plane, wb);
-      for (int s = 0; s < steps; s += 3) {
-        load_chunk<LAYOUT, CW>(row_ptr(s + 2), plane, wc);
-        step(wa, s);
-        if (s + 1 >= steps) break;
-        load_chunk<LAYOUT, CW>(row_ptr(s + 3), plane, wa);
-        step(wb, s + 1);
-        if (s + 2 >= steps) break;
-        load_chunk<LAYOUT, CW>(row_ptr(s + 4), plane, wb);
-        step(wc, s + 2);
-      }
-#else
+      // rows of step s + 1 loaded while step s is processed
       const uint8_t* rb = tbase;
       auto row_ptr = [&](int s) -> const uint8_t* {
         if (FULL) return rb + voff;
         return s < vsteps ? pf + (int64_t)s * rowstep : pf;
       };
+      auto row_ptr_b = [&](int s) -> const uint8_t* {
+        if (FULL) return rb + hb + voff;
+        return s < vstepsb ? pf + hb + (int64_t)s * rowstep : pf;
+      };
       uint32_t wa[CW], wb[CW];
-      load_chunk<LAYOUT, CW>(row_ptr(0), plane, wa);
+      load_chunk<LAYOUT, CW>(row_ptr(0), row_ptr_b(0), plane, wa);
       for (int s = 0; s < steps; s += 2) {
         if (FULL && s + 1 < steps) rb += rowstep;
-        load_chunk<LAYOUT, CW>(row_ptr(s + 1), plane, wb);
+        load_chunk<LAYOUT, CW>(row_ptr(s + 1), row_ptr_b(s + 1), plane, wb);
         step(wa, s);
         if (s + 1 >= steps) break;
         if (FULL && s + 2 < steps) rb += rowstep;
-        load_chunk<LAYOUT, CW>(row_ptr(s + 2), plane, wa);
+        load_chunk<LAYOUT, CW>(row_ptr(s + 2), row_ptr_b(s + 2), plane, wa);
         step(wb, s + 1);
       }
-#endif
     };
     if (full) run(std::true_type{});
     else run(std::false_type{});
@@ -673,13 +680,18 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     for (int rr = 0; rr < NR; ++rr) {
       const int sh = 8 * rr;
       const uint32_t c = ((rr & 1) ? (CumB >> ((rr >> 1) * 16)) : (CumA >> ((rr >> 1) * 16))) & 0xFFFFu;
-      uint32_t wx = (O >> sh) & 0xFFu;
+      uint32_t wx = (O >> sh) & 0xFFu, nb2 = 0;  // nb2: pixels of the second pieces (rows + half)
 #pragma unroll
-      for (int i = 1; i < CW; ++i) wx += 2u * (uint32_t)i * ((P[i] >> sh) & 0xFFu);
+      for (int i = 1; i < CW; ++i) wx += xoff(i) * ((P[i] >> sh) & 0xFFu);
+      if (SPLIT) {
+#pragma unroll
+        for (int i = 4; i < CW; ++i) nb2 += (P[i] >> sh) & 0xFFu;
+      }
       const uint32_t qq = ((rr & 1) ? (Qb >> ((rr >> 1) * 16)) : (Qa >> ((rr >> 1) * 16))) & 0xFFFFu;
       acc[3 * rr + 0] = c + xacc[3 * rr + 0];
       acc[3 * rr + 1] = x0 * c + wx + xacc[3 * rr + 1];
-      acc[3 * rr + 2] = (uint32_t)y0 * c + (uint32_t)g.k * ((uint32_t)steps * c - qq) + xacc[3 * rr + 2];
+      acc[3 * rr + 2] = (uint32_t)y0 * c + (uint32_t)g.rstep * ((uint32_t)steps * c - qq) +
+                        (uint32_t)half * nb2 + xacc[3 * rr + 2];
     }
     wave_sums<3 * NR>(acc);
     if (lane == 63) {
@@ -880,11 +892,15 @@ int build_chroma_tables(const RangeTables* t, ChromaTables* ct, hipStream_t s) {
   return hipGetLastError();
 }
 
-// Column chunks of 2*kChunkWords pixels; k rows per step, as many as fit a
-// kHotLanes-lane workgroup, rounded down to whole waves when that keeps >= 7/8 of
-// the lanes (the kernel's uniform fast path needs whole waves).
+// Chunk columns of 8 (YUYV: one 16-byte piece of each of two rows) or
+// 2*kChunkWords (ov7670) pixels; k rows per half step, as many as fit a
+// kHotLanes-lane workgroup, rounded down to whole waves when that keeps >= 7/8
+// of the lanes (the kernel's uniform fast path needs whole waves).
 bool chroma_geometry(const KernelArgs& a, ChromaGeom& g) {
-  const int px = 2 * kChunkWords;
+  const bool split = a.layout == TRIK_HSV_LAYOUT_YUYV;
+  // rows of more than kHotLanes pieces: the two pieces from the two halves of one row
+  const bool wide = split && a.width / 8 > kHotLanes;
+  const int px = split ? (wide ? 16 : 8) : 2 * kChunkWords;
   if (a.width <= 0 || a.width % px || a.height <= 0) return false;
   const int cpr = a.width / px;
   if (cpr > kHotLanes) return false;
@@ -896,13 +912,17 @@ bool chroma_geometry(const KernelArgs& a, ChromaGeom& g) {
     if ((kk * cpr) % 64 == 0) { k = kk; break; }
   g.cpr = cpr;
   g.k = k;
-  const int steps_total = (a.height + k - 1) / k;
+  g.dy = split && !wide ? k : 0;
+  g.dx = wide ? a.width / 2 : 0;
+  g.rstep = k + g.dy;
+  const int steps_total = (a.height + g.rstep - 1) / g.rstep;
   g.tiles_per_frame = (steps_total + kMaxSteps - 1) / kMaxSteps;
   g.steps = (steps_total + g.tiles_per_frame - 1) / g.tiles_per_frame;
   g.n_tiles = (int64_t)g.tiles_per_frame * a.n_frames;
   // per drain round a lane adds <= 2 pixels: byte counts <= 2r, x sums <= 2r*W,
   // row sums <= 2r*rows; the 16-bit sums must take at least one round
-  const int span = a.width > g.steps * k ? a.width : g.steps * k;
+  const int rows = g.steps * g.rstep;
+  const int span = a.width > rows ? a.width : rows;
   if (2LL * span > 65535) return false;
   int r = 65535 / (2 * span);
   g.flush_rounds = r > 127 ? 127 : r;
