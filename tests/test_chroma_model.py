@@ -76,49 +76,84 @@ def cost(d):
     return np.where(d == KEXC, 65536, np.where(b1 <= b2 + 1, 0, L * (512 - L)))
 
 
+def first_nonzero(P):
+    """first_nz: the first Y with a nonzero mask (256: all zero)."""
+    nz = P != 0
+    return np.where(nz.any(1), np.argmax(nz, axis=1), 256)
+
+
 def build(P):
-    """chroma_block_kernel: per 16-chroma block the cheapest (M1, M2)."""
-    S = summaries(P)
-    n, v1, v2 = S[0], S[1], S[2]
-    present = np.ones(65536, np.int64)
-    present |= np.where(n > 0, 1 << v1, 0)
-    present |= np.where(n == 2, 1 << v2, 0)
+    """chroma_summary_kernel + chroma_block_kernel + chroma_palette_kernel:
+    per 16-chroma block the cheapest (cost, M1 | M2 << 4, cut A), ties by the
+    smaller pair, then the smaller cut; A is 0 or the first nonzero Y of one of
+    the block's chromas.  A chroma whose profile starts at A is described from
+    A on (its leading zero run dropped), one that starts above A as before, one
+    that starts below A is an exception."""
+    N = P.shape[0]
+    f = first_nonzero(P)
+    Y = np.arange(256)[None, :]
+    Pd = np.where(Y < f[:, None], P[np.arange(N), np.minimum(f, 255)][:, None], P)
+    Sf, Sd = summaries(P), summaries(Pd)
+    fb = f.reshape(4096, 16)
+
+    def descs(k, A):  # A: per-chroma cut
+        df = desc(Sf, np.full(N, k & 15), np.full(N, k >> 4))
+        dd = desc(Sd, np.full(N, k & 15), np.full(N, k >> 4))
+        return np.where(f > A, df, np.where(f == A, dd, KEXC))
+
+    def choose(pairs, block_ok):
+        best = np.full(4096, np.iinfo(np.int64).max)
+        for k in pairs:
+            ok = block_ok(k)
+            for j in range(-1, 16):
+                A = np.zeros(4096, np.int64) if j < 0 else fb[:, j]
+                if j >= 0:
+                    valid = (A > 0) & (A < 256)
+                c = cost(descs(k, np.repeat(A, 16))).reshape(4096, 16).sum(1)
+                key = (c << 17) | (k << 9) | A
+                take = ok & (key < best) if j < 0 else ok & valid & (key < best)
+                best[take] = key[take]
+        return best
+
+    present = np.ones(N, np.int64)
+    for S in (Sf, Sd):
+        present |= np.where(S[0] > 0, 1 << S[1], 0)
+        present |= np.where(S[0] == 2, 1 << S[2], 0)
     present = np.bitwise_or.reduce(present.reshape(4096, 16), axis=1)
-    best = np.full(4096, np.iinfo(np.int64).max)
-    best_k = np.zeros(4096, np.int64)
-    for k in range(256):
-        M1, M2 = k & 15, k >> 4
-        ok = ((present >> M1) & 1).astype(bool) & ((present >> M2) & 1).astype(bool)
-        c = cost(desc(S, np.full(65536, M1), np.full(65536, M2))).reshape(4096, 16).sum(1)
-        better = ok & (c < best)
-        best[better] = c[better]
-        best_k[better] = k
-    # chroma_palette_kernel: the 32 most used pairs (ties: smaller k); a block
-    # whose pair missed the palette takes the cheapest palette pair
+    best = choose(range(256), lambda k: ((present >> (k & 15)) & (present >> (k >> 4)) & 1).astype(bool))
+    best_k = (best >> 9) & 255
+    # chroma_palette_kernel: the 32 most used pairs (ties: smaller k); then the
+    # choice among the palette's pairs (the same where the pair made it)
     hist = np.bincount(best_k, minlength=256)
     order = sorted(range(256), key=lambda k: (-hist[k], k))
     palette = [k for k in order[:32] if hist[k] > 0]
-    miss = ~np.isin(best_k, palette)
-    if miss.any():
-        costs = np.stack([cost(desc(S, np.full(65536, k & 15), np.full(65536, k >> 4))).reshape(4096, 16).sum(1)
-                          for k in palette], axis=1)
-        best_k = np.where(miss, np.asarray(palette)[np.argmin(costs, axis=1)], best_k)
-    kk = np.repeat(best_k, 16)
-    return desc(S, kk & 15, kk >> 4), best_k
+    best = choose(palette, lambda k: np.ones(4096, bool))
+    best_k, best_A = (best >> 9) & 255, best & 511
+    return descs_for(best_k, best_A, descs), best_k, best_A
 
 
-@pytest.mark.parametrize("n_ranges,max_words", [(4, 0.065), (1, 0.005)])
+def descs_for(best_k, best_A, descs):
+    runs = np.zeros(65536, np.int64)
+    kk, AA = np.repeat(best_k, 16), np.repeat(best_A, 16)
+    for k in np.unique(best_k):
+        sel = kk == k
+        runs[sel] = descs(k, AA)[sel]
+    return runs
+
+
+@pytest.mark.parametrize("n_ranges,max_words", [(4, 0.03), (1, 0.005)])
 def test_descriptors_exact_on_all_triples(oracle_mod, n_ranges, max_words):
     P = profiles(oracle_mod, BENCH[:n_ranges])
-    runs, blocks = build(P)
+    runs, blocks, cut = build(P)
     Y = np.arange(256)[None, :]
     b1, b2 = (runs & 255)[:, None], (runs >> 8)[:, None]
-    kk = np.repeat(blocks, 16)
-    M1, M2 = (kk & 15)[:, None], (kk >> 4)[:, None]
+    kk, AA = np.repeat(blocks, 16), np.repeat(cut, 16)
+    M1, M2, A = (kk & 15)[:, None], (kk >> 4)[:, None], AA[:, None]
     x = (runs == KEXC)[:, None]
-    lt, le = Y < b1, (Y <= b2) & ~x
-    fast = np.where(le, np.where(lt, M1, M2), 0)
+    lt, le, ge = Y < b1, (Y <= b2) & ~x, Y >= A
+    fast = np.where(le & ge, np.where(lt, M1, M2), 0)
     flagged = x | (lt & (Y > b2))
+    assert not (flagged & ~ge & ~x).any()                 # windows lie above the cut
     assert (fast[flagged] == 0).all()                     # the exact path adds these
     assert np.array_equal(np.where(flagged, P, fast), P)  # everything else is exact
     words = (1 - (1 - flagged.mean(1)) ** 2).mean()       # a word: two uniform Y of one chroma
