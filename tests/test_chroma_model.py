@@ -105,6 +105,8 @@ def build(P):
         best = np.full(4096, np.iinfo(np.int64).max)
         for k in pairs:
             ok = block_ok(k)
+            if not ok.any():
+                continue
             for j in range(-1, 16):
                 A = np.zeros(4096, np.int64) if j < 0 else fb[:, j]
                 if j >= 0:
