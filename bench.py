@@ -137,9 +137,8 @@ def main():
     first, count = frame_shard(world * F, rank, world)  # weak scaling: F frames per rank
     assert count == F
     trik_hsv.synth(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, args.kind, SEED, first_frame=first)
-    det = trik_hsv.Detector()
-    trik_hsv.set_hot_kernel({"auto": trik_hsv.HOT_AUTO, "stripe": trik_hsv.HOT_STRIPE,
-                             "chroma": trik_hsv.HOT_CHROMA}[args.hot])
+    det = trik_hsv.Detector(hot={"auto": trik_hsv.HOT_AUTO, "stripe": trik_hsv.HOT_STRIPE,
+                                 "chroma": trik_hsv.HOT_CHROMA}[args.hot])
     sums = torch.zeros((F, T, 3), dtype=torch.int64, device=dev)
 
     def step(ev0=None, ev1=None):
@@ -170,7 +169,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
     kname = {trik_hsv.HOT_CHROMA: "chroma_kernel", trik_hsv.HOT_STRIPE: "stripe_kernel",
-             trik_hsv.HOT_GENERIC: "reduce_kernel"}.get(trik_hsv.last_hot_kernel(), "?")
+             trik_hsv.HOT_GENERIC: "reduce_kernel"}.get(det.last_hot_kernel(), "?")
 
     el = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:

@@ -386,28 +386,32 @@ int32_t trik_hsv_batch_sums(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvFra
                             const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int32_t n_ranges,
                             TrikHsvTargetSums* sums_dev, void* hip_stream);
 
-/* Hot-kernel selection for trik_hsv_batch_sums / _process_batch / _masks
- * (process-wide; for tests and A/B runs).  TRIK_HSV_HOT_AUTO picks the
- * chroma-run kernel for batches of at least TRIK_HSV_CHROMA_MIN_PIXELS pixels
- * whose geometry it takes and whose range set sends at most
- * TRIK_HSV_CHROMA_MAX_SHARE of the words to its exact path (see
- * trik_hsv_chroma_share), the stripe kernel otherwise; the two give the same
- * results.  Returns the previous setting, or -1 for an unknown kind. */
+/* Hot-kernel selection of one handle for its trik_hsv_batch_sums /
+ * _process_batch / _masks / _blob_batch calls and process() (tests and A/B
+ * runs; other handles are not affected).  TRIK_HSV_HOT_AUTO (the default)
+ * picks the chroma-run kernel for batches of at least
+ * TRIK_HSV_CHROMA_MIN_PIXELS pixels whose geometry it takes and whose range
+ * set sends at most TRIK_HSV_CHROMA_MAX_SHARE of the words to its exact path
+ * (see trik_hsv_chroma_share), the stripe kernel otherwise; the two give the
+ * same results.  The first batch with a new range set is not held up by that
+ * share: both kernels are enqueued and the device runs the one the rule picks.
+ * Returns the previous setting, or -1 for a NULL handle or an unknown kind. */
 #define TRIK_HSV_HOT_AUTO 0
 #define TRIK_HSV_HOT_STRIPE 1
 #define TRIK_HSV_HOT_CHROMA 2
 #define TRIK_HSV_HOT_GENERIC 3
 #define TRIK_HSV_CHROMA_MIN_PIXELS (32 * 640 * 480)
 #define TRIK_HSV_CHROMA_MAX_SHARE 0.25
-int32_t trik_hsv_set_hot_kernel(int32_t kind);
+int32_t trik_hsv_set_hot_kernel(TRIK_VIDTRANSCODE_CV_Handle handle, int32_t kind);
 /* The chroma-run kernel's expected exact-path word share (uniform input) for
  * the handle's current batched-sums range set (the maximum over its groups of
- * 4 ranges), or -1 when its tables are not built yet.  Returns 0 or
- * TRIK_IVIDTRANSCODE_EFAIL. */
+ * 4 ranges), or -1 when its tables are not built.  Waits for the builder's
+ * readback if it is still in flight.  Returns 0 or TRIK_IVIDTRANSCODE_EFAIL. */
 int32_t trik_hsv_chroma_share(TRIK_VIDTRANSCODE_CV_Handle handle, double* share);
-/* The kernel the last hot launch on this thread ran (TRIK_HSV_HOT_STRIPE,
- * _CHROMA or _GENERIC; 0 before any). */
-int32_t trik_hsv_last_hot_kernel(void);
+/* The kernel the handle's last hot launch ran (TRIK_HSV_HOT_STRIPE, _CHROMA or
+ * _GENERIC; 0 before any).  When the device chose (see above) this waits for
+ * the builder's readback. */
+int32_t trik_hsv_last_hot_kernel(TRIK_VIDTRANSCODE_CV_Handle handle);
 
 /* Epilogue only: sums_dev -> targets_dev for an n_frames x n_ranges grid. */
 int32_t trik_hsv_batch_targets(const TrikHsvFrameBatch* batch, int32_t n_ranges,

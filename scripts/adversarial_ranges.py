@@ -40,7 +40,7 @@ def main():
         sums = torch.zeros((F, len(ranges), 3), dtype=torch.int64, device=dev)
         line = [f"{name:16s}"]
         for hot in (trik_hsv.HOT_CHROMA, trik_hsv.HOT_STRIPE, trik_hsv.HOT_AUTO):
-            trik_hsv.set_hot_kernel(hot)
+            det.set_hot_kernel(hot)
             det.batch_sums(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, ranges, sums, stream=stream)
             if hot == trik_hsv.HOT_CHROMA:
                 line.append(f"flagged {det.chroma_flagged_share():.3f}")
@@ -51,10 +51,10 @@ def main():
                 det.batch_sums(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, ranges, sums, stream=stream)
             e1.record(stream)
             torch.cuda.synchronize()
-            ran = {trik_hsv.HOT_CHROMA: "chroma", trik_hsv.HOT_STRIPE: "stripe"}.get(trik_hsv.last_hot_kernel(), "?")
+            ran = {trik_hsv.HOT_CHROMA: "chroma", trik_hsv.HOT_STRIPE: "stripe"}.get(det.last_hot_kernel(), "?")
             line.append(f"{['auto', 'stripe', 'chroma', 'generic'][hot] if hot < 4 else hot}->{ran} "
                         f"{e0.elapsed_time(e1) / 5:.3f} ms")
-        trik_hsv.set_hot_kernel(trik_hsv.HOT_AUTO)
+        det.close()
         print("  ".join(line), flush=True)
 
 

@@ -1,5 +1,5 @@
 """GPU time of trik_hsv_blob_batch (4096 ov7670 VGA frames, scene or uniform)
-for A/B runs of library variants (TRIK_HSV_LIB).  usage: python scripts/blob_time.py [frames] [kind]"""
+of the in-tree library.  usage: python scripts/blob_time.py [frames] [kind]"""
 import os
 import sys
 
@@ -25,4 +25,4 @@ for _ in range(10):
     det.blob_batch(dev, W, H, W, RED, stream=s)
 b.record(s)
 torch.cuda.synchronize()
-print(f"{os.environ.get('TRIK_HSV_LIB', 'default').split('/')[-2]} frames {F} kind {kind}: {a.elapsed_time(b) / 10:.3f} ms")
+print(f"frames {F} kind {kind}: {a.elapsed_time(b) / 10:.3f} ms")

@@ -109,7 +109,7 @@ int main(int argc, char** argv) {
   for (size_t i = 0; i < libs.size(); ++i) {
     Lib& L = libs[i];
     if (L.create(nullptr, &L.h)) return 2;
-    L.set_hot(hot);
+    L.set_hot(L.h, hot);
     CK(hipMemsetAsync(d_sums, 0, sb, s));
     if (L.sums(L.h, &b, all, T, d_sums, s)) {
       fprintf(stderr, "%s: %s\n", L.path.c_str(), L.last_error());
@@ -128,7 +128,7 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   for (int r = 0; r < rounds; ++r)
     for (Lib& L : libs) {
-      L.set_hot(hot);
+      L.set_hot(L.h, hot);
       for (int w = 0; w < 3; ++w) L.sums(L.h, &b, all, T, d_sums, s);
       for (int k = 0; k < iters; ++k) {
         CK(hipEventRecord(e0, s));

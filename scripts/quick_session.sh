@@ -3,7 +3,7 @@
 # at the first fault / timeout.  usage: bash scripts/quick_session.sh TAG [--no-pmc]
 set -u
 cd "$GRAFT_REPO_ROOT"; OUT="$GRAFT_REPO_ROOT/gpurun_out"; TAG="${1:-q}"; mkdir -p "$OUT"
-timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > "$OUT/gpu_tests_$TAG.log" 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/gpu_tests_$TAG.log" 2>&1
 rc=$?; echo "[q] tests rc=$rc"; tail -3 "$OUT/gpu_tests_$TAG.log"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python bench.py --no-cpu-baseline > "$OUT/bench_$TAG.log" 2>&1

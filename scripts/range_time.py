@@ -1,4 +1,4 @@
-"""Auto-range batch timing on two inputs (development A/B; TRIK_HSV_LIB picks a
+"""Auto-range batch timing on two inputs (development timing of the in-tree
 library variant): the synthetic scene of bench_operator.py and uniform random
 bytes (every lane of a wave on its own H/S/V bin -- the worst case for the
 wave-peeled histogram atomics).  usage: python scripts/range_time.py [--frames N]"""
@@ -19,7 +19,7 @@ def main():
     import trik_hsv
     W, H, LL, F = 640, 480, 1280, args.frames
     dev = torch.empty(F * H * LL, dtype=torch.uint8, device="cuda")
-    out = {"lib": os.environ.get("TRIK_HSV_LIB", "default")}
+    out = {"lib": "in-tree"}
     for name in ("scene", "random"):
         if name == "scene":
             trik_hsv.synth(dev, W, H, LL, trik_hsv.LAYOUT_YUYV, 1, 0x7A1C)

@@ -65,16 +65,14 @@ def test_blob_batch_vs_oracle(hsv, oracle_mod, geom, hot):
     cases = CASES if w * h <= 640 * 480 else CASES[2:4]
     frames = _frames(oracle_mod, w, h, ll, cases)
     dev = torch.from_numpy(np.concatenate(frames)).cuda()
-    det = hsv.Detector()
-    prev = hsv.set_hot_kernel(hsv.HOT_CHROMA if hot == "chroma" else hsv.HOT_AUTO)
+    det = hsv.Detector(hot=hsv.HOT_CHROMA if hot == "chroma" else hsv.HOT_AUTO)
     try:
         res = det.blob_batch(dev, w, h, ll, RED, meta=True, labels=True)
         chroma_ok = hot == "chroma" and w % 16 == 0 and ll % 16 == 0
-        assert hsv.last_hot_kernel() == (hsv.HOT_CHROMA if chroma_ok else hsv.HOT_STRIPE)
+        assert det.last_hot_kernel() == (hsv.HOT_CHROMA if chroma_ok else hsv.HOT_STRIPE)
         for i, fr in enumerate(frames):
             _check(oracle_mod, res, i, fr, w, h, ll, RED, (geom, cases[i]))
     finally:
-        hsv.set_hot_kernel(prev)
         det.close()
 
 
@@ -90,15 +88,13 @@ def test_blob_batch_auto_chroma_bitmap(hsv, oracle_mod):
     frames = _frames(oracle_mod, w, h, ll, cases)
     dev = torch.from_numpy(np.concatenate(frames)).cuda()
     det = hsv.Detector()
-    prev = hsv.set_hot_kernel(hsv.HOT_AUTO)
     try:
         for rng_hsv in (RED, (120, 40, 50, 50, 60, 40)):
             res = det.blob_batch(dev, w, h, ll, rng_hsv, meta=True, labels=True)
-            assert hsv.last_hot_kernel() == hsv.HOT_CHROMA
+            assert det.last_hot_kernel() == hsv.HOT_CHROMA
             for i, fr in enumerate(frames):
                 _check(oracle_mod, res, i, fr, w, h, ll, rng_hsv, (rng_hsv, cases[i]))
     finally:
-        hsv.set_hot_kernel(prev)
         det.close()
 
 

@@ -1,6 +1,6 @@
 """GPU parity of the chroma-run hot kernel (trik_hsv_chroma.hip) against the
 CPU oracle, bit-exact, through the C ABI with the kernel forced by
-trik_hsv.set_hot_kernel(HOT_CHROMA).
+Detector.set_hot_kernel(HOT_CHROMA).
 
 The kernel resolves most YUYV words from per-chroma run descriptors; the
 pixels inside a chroma's window, and both pixels of exception-code chromas,
@@ -18,6 +18,8 @@ from gpu_util import (BENCH_RANGES, LAYOUT_OV7670, LAYOUT_YUYV, T0, T1,
 from test_gpu_parity import EDGE_RANGES
 
 pytestmark = pytest.mark.gpu
+
+HOT_CHROMA = 2  # trik_hsv.HOT_CHROMA (the package is imported by the fixtures)
 
 
 @pytest.fixture(scope="module")
@@ -44,10 +46,11 @@ def detector(hsv, torch_dev):
 
 
 @pytest.fixture()
-def chroma(hsv):
-    prev = hsv.set_hot_kernel(hsv.HOT_CHROMA)
-    yield hsv
-    hsv.set_hot_kernel(prev)
+def chroma(hsv, detector):
+    """The module's detector with the chroma-run kernel forced."""
+    prev = detector.set_hot_kernel(hsv.HOT_CHROMA)
+    yield detector
+    detector.set_hot_kernel(prev)
 
 
 def _to_dev(torch, arr):
@@ -63,7 +66,7 @@ def test_chroma_exhaustive_all_yuv_triples(torch_dev, detector, oracle_mod, chro
     frame, w, h, ll = exhaustive_yuyv_frame()
     _, want = oracle_mod.frame(frame, w, h, ll, LAYOUT_YUYV, ranges, want_mask=True)
     masks, sums = detector.batch_masks(_to_dev(torch, frame), w, h, ll, LAYOUT_YUYV, ranges)
-    assert chroma.last_hot_kernel() == chroma.HOT_CHROMA
+    assert chroma.last_hot_kernel() == HOT_CHROMA
     got = masks[0].cpu().numpy()
     bad = np.count_nonzero(got != want)
     assert bad == 0, f"{bad} pixels differ; first at {np.argwhere(got != want)[:5].tolist()}"
@@ -79,7 +82,7 @@ def test_chroma_exhaustive_ov7670(torch_dev, detector, oracle_mod, chroma):
     planar = np.concatenate([ylum.reshape(-1), chrom.reshape(-1)])
     _, want = oracle_mod.frame(planar, w, h, w, LAYOUT_OV7670, BENCH_RANGES, want_mask=True)
     masks, sums = detector.batch_masks(_to_dev(torch, planar), w, h, w, LAYOUT_OV7670, BENCH_RANGES)
-    assert chroma.last_hot_kernel() == chroma.HOT_CHROMA
+    assert chroma.last_hot_kernel() == HOT_CHROMA
     assert np.array_equal(masks[0].cpu().numpy(), want)
     assert sums[0].cpu().numpy().tolist() == sums_from_mask(want, 4).tolist()
 
@@ -105,7 +108,7 @@ def test_chroma_batch_vs_oracle(torch_dev, hsv, detector, oracle_mod, chroma, w,
     host = oracle_mod.synth(n, w, h, ll, layout, kind, 0x7A1C, first_frame=100)
     assert np.array_equal(dev.cpu().numpy(), host)
     sums, tg = detector.process_batch(dev, w, h, ll, layout, ranges)
-    assert hsv.last_hot_kernel() == hsv.HOT_CHROMA
+    assert detector.last_hot_kernel() == hsv.HOT_CHROMA
     want_s, want_t = oracle_mod.batch(host, fb, n, w, h, ll, layout, ranges, n_threads=8)
     assert np.array_equal(sums.cpu().numpy(), want_s)
     assert np.array_equal(tg[:, :, :3].cpu().numpy(), want_t)
@@ -124,7 +127,7 @@ def test_chroma_padded_and_strided(torch_dev, hsv, detector, oracle_mod, chroma)
         ranges = BENCH_RANGES + EDGE_RANGES[:2]
         sums, tg = detector.process_batch(_to_dev(torch, host), w, h, ll, lay, ranges, n_frames=n,
                                           frame_stride=stride)
-        assert hsv.last_hot_kernel() == hsv.HOT_CHROMA, (w, h, ll, lay)
+        assert detector.last_hot_kernel() == hsv.HOT_CHROMA, (w, h, ll, lay)
         want_s, want_t = oracle_mod.batch(host, stride, n, w, h, ll, lay, ranges)
         assert np.array_equal(sums.cpu().numpy(), want_s), (w, h, ll, lay)
         assert np.array_equal(tg[:, :, :3].cpu().numpy(), want_t), (w, h, ll, lay)
@@ -134,7 +137,7 @@ def test_chroma_padded_and_strided(torch_dev, hsv, detector, oracle_mod, chroma)
     buf = np.zeros(host.size + 1, np.uint8)
     buf[1:] = host
     sums, _ = detector.process_batch(_to_dev(torch, buf)[1:], w, h, ll, LAYOUT_YUYV, [T0], n_frames=2)
-    assert hsv.last_hot_kernel() == hsv.HOT_GENERIC
+    assert detector.last_hot_kernel() == hsv.HOT_GENERIC
     want_s, _ = oracle_mod.batch(host, h * ll, 2, w, h, ll, LAYOUT_YUYV, [T0])
     assert np.array_equal(sums.cpu().numpy(), want_s)
 
@@ -153,40 +156,41 @@ def test_chroma_range_set_changes(torch_dev, hsv, detector, oracle_mod, chroma):
         assert np.array_equal(sums.cpu().numpy(), want), ranges
 
 
-def test_chroma_equals_stripe_on_full_c3(torch_dev, hsv, detector, oracle_mod):
+def test_chroma_equals_stripe_on_full_c3(torch_dev, hsv, oracle_mod):
     """The bench workload (4096 x 640x480, T=4): AUTO picks the chroma kernel,
-    its sums equal the stripe kernel's for every frame, and sampled frames
-    equal the oracle."""
+    its sums and targets equal the stripe kernel's for every frame, and 512 of
+    its frames (the first and the last 256) equal the oracle."""
     torch = torch_dev
     w, h, ll, n = 640, 480, 1280, 4096
     dev = torch.empty(n * h * ll, dtype=torch.uint8, device="cuda")
     hsv.synth(dev, w, h, ll, LAYOUT_YUYV, 0, 0x7A1C)
-    prev = hsv.set_hot_kernel(hsv.HOT_AUTO)
+    d = hsv.Detector()
     try:
-        s_auto, t_auto = detector.process_batch(dev, w, h, ll, LAYOUT_YUYV, BENCH_RANGES)
-        assert hsv.last_hot_kernel() == hsv.HOT_CHROMA
-        hsv.set_hot_kernel(hsv.HOT_STRIPE)
-        s_str, t_str = detector.process_batch(dev, w, h, ll, LAYOUT_YUYV, BENCH_RANGES)
-        assert hsv.last_hot_kernel() == hsv.HOT_STRIPE
+        s_auto, t_auto = d.process_batch(dev, w, h, ll, LAYOUT_YUYV, BENCH_RANGES)
+        assert d.last_hot_kernel() == hsv.HOT_CHROMA
+        d.set_hot_kernel(hsv.HOT_STRIPE)
+        s_str, t_str = d.process_batch(dev, w, h, ll, LAYOUT_YUYV, BENCH_RANGES)
+        assert d.last_hot_kernel() == hsv.HOT_STRIPE
     finally:
-        hsv.set_hot_kernel(prev)
+        d.close()
     assert torch.equal(s_auto, s_str) and torch.equal(t_auto, t_str)
-    s = s_auto.cpu().numpy()
-    for f in (0, 1, 2047, 4095):
-        host = oracle_mod.synth(1, w, h, ll, LAYOUT_YUYV, 0, 0x7A1C, first_frame=f)
-        want, _ = oracle_mod.frame(host, w, h, ll, LAYOUT_YUYV, BENCH_RANGES)
-        assert np.array_equal(s[f], want), f
+    s, t = s_auto.cpu().numpy(), t_auto.cpu().numpy()
+    for first in (0, n - 256):
+        host = oracle_mod.synth(256, w, h, ll, LAYOUT_YUYV, 0, 0x7A1C, first_frame=first)
+        want_s, want_t = oracle_mod.batch(host, h * ll, 256, w, h, ll, LAYOUT_YUYV, BENCH_RANGES, n_threads=16)
+        assert np.array_equal(s[first:first + 256], want_s), first
+        assert np.array_equal(t[first:first + 256, :, :3], want_t), first
 
 
-def test_auto_keeps_small_batches_on_stripe(torch_dev, hsv, detector):
+def test_auto_keeps_small_batches_on_stripe(torch_dev, hsv):
     torch = torch_dev
     dev = torch.zeros(4 * 480 * 1280, dtype=torch.uint8, device="cuda")
-    prev = hsv.set_hot_kernel(hsv.HOT_AUTO)
+    d = hsv.Detector()
     try:
-        detector.process_batch(dev, 640, 480, 1280, LAYOUT_YUYV, [T0])
-        assert hsv.last_hot_kernel() == hsv.HOT_STRIPE
+        d.process_batch(dev, 640, 480, 1280, LAYOUT_YUYV, [T0])
+        assert d.last_hot_kernel() == hsv.HOT_STRIPE
     finally:
-        hsv.set_hot_kernel(prev)
+        d.close()
 
 
 # range sets whose profiles have several separate runs per chroma: most words
@@ -203,7 +207,7 @@ def test_chroma_exhaustive_adversarial(torch_dev, detector, oracle_mod, chroma, 
     frame, w, h, ll = exhaustive_yuyv_frame()
     _, want = oracle_mod.frame(frame, w, h, ll, LAYOUT_YUYV, ranges, want_mask=True)
     masks, sums = detector.batch_masks(_to_dev(torch, frame), w, h, ll, LAYOUT_YUYV, ranges)
-    assert chroma.last_hot_kernel() == chroma.HOT_CHROMA
+    assert chroma.last_hot_kernel() == HOT_CHROMA
     assert detector.chroma_flagged_share() > 0.5
     got = masks[0].cpu().numpy()
     assert np.array_equal(got, want), f"{np.count_nonzero(got != want)} pixels differ"
@@ -219,17 +223,15 @@ def test_auto_share_guard(torch_dev, hsv, oracle_mod):
     dev = torch.empty(n * h * ll, dtype=torch.uint8, device="cuda")
     hsv.synth(dev, w, h, ll, LAYOUT_YUYV, 0, 0x7A1C, first_frame=9)
     host = dev.cpu().numpy()
-    prev = hsv.set_hot_kernel(hsv.HOT_AUTO)
     d = hsv.Detector()
     try:
         assert d.chroma_flagged_share() == -1.0
         for ranges, kernel, lo, hi in ((BENCH_RANGES, hsv.HOT_CHROMA, 0.02, 0.04),
                                        (S_BANDS, hsv.HOT_STRIPE, 0.5, 0.7)):
             sums, _ = d.process_batch(dev, w, h, ll, LAYOUT_YUYV, ranges)
-            assert hsv.last_hot_kernel() == kernel
+            assert d.last_hot_kernel() == kernel
             assert lo < d.chroma_flagged_share() < hi
             want, _ = oracle_mod.batch(host, h * ll, n, w, h, ll, LAYOUT_YUYV, ranges, n_threads=8)
             assert np.array_equal(sums.cpu().numpy(), want)
     finally:
         d.close()
-        hsv.set_hot_kernel(prev)

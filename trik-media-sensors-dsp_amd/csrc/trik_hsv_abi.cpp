@@ -127,31 +127,96 @@ std::string validate_batch(const TrikHsvFrameBatch* b) {
 // ---------------------------------------------------------------------------
 // Handle
 // ---------------------------------------------------------------------------
+// Device buffers a handle shares between calls that may run on different
+// streams: the last use on each stream is an event, so that a later call can
+// make its stream wait for them (device side) or, before the buffer is
+// rewritten, find out without blocking whether they have finished.
+struct StreamUses {
+  std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
+  // the calling stream has (just) enqueued work that reads or writes the buffer
+  int32_t note(hipStream_t s) {
+    for (auto& u : uses)
+      if (u.first == s) return (int32_t)hipEventRecord(u.second, s);
+    hipEvent_t e = nullptr;
+    hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    if (r != hipSuccess) return (int32_t)r;
+    uses.emplace_back(s, e);
+    return (int32_t)hipEventRecord(e, s);
+  }
+  // every recorded use has completed (non-blocking)
+  bool idle() const {
+    for (const auto& u : uses)
+      if (hipEventQuery(u.second) != hipSuccess) return false;
+    return true;
+  }
+  // stream s waits (device side) for the uses on other streams
+  int32_t order_after(hipStream_t s) const {
+    for (const auto& u : uses)
+      if (u.first != s) {
+        hipError_t r = hipStreamWaitEvent(s, u.second, 0);
+        if (r != hipSuccess) return (int32_t)r;
+      }
+    return 0;
+  }
+  void wait_all() const {
+    for (const auto& u : uses) (void)hipEventSynchronize(u.second);
+  }
+  void release() {
+    for (auto& u : uses) (void)hipEventDestroy(u.second);
+    uses.clear();
+  }
+};
+
 // Compiled range tables (device) for one range set, with the key (packed
-// bounds) they were compiled from and their pinned staging.
+// bounds) they were compiled from and their pinned staging.  A handle keeps a
+// few of them (LRU), so that alternating range sets -- the batched sums, the
+// preview's single range, the multi-blob sensor's sticky range -- do not
+// recompile, and a new range set never overwrites tables a queued kernel is
+// still reading: it takes a set whose uses have all completed.
 struct TableSet {
-  RangeTables* d_tables = nullptr;
+  std::vector<uint32_t> key;  // empty: unused
   int groups_cap = 0;
-  std::vector<uint32_t> key;
+  RangeTables* d_tables = nullptr;
   RangeTables* h_tables = nullptr;
   StripeTables* d_stripe = nullptr;
   StripeTables* h_stripe = nullptr;
-  ChromaTables* d_chroma = nullptr;  // built on first use per range set (chroma-run kernel)
+  ChromaTables* d_chroma = nullptr;        // built on first use per range set (chroma-run kernel)
+  unsigned long long* h_cost = nullptr;    // pinned readback of each group's flagged_cost
   bool chroma_built = false;
-  double chroma_share = -1.0;  // the builder's expected exact-path word share (max over groups)
+  double chroma_share = -1.0;  // the builder's expected exact-path word share (max over groups), once read
+  hipEvent_t ready = nullptr;       // uploads (and the chroma build) enqueued before it
+  hipEvent_t cost_ready = nullptr;  // the flagged_cost readback enqueued before it
+  StreamUses users;                 // kernels that read the set
+  uint64_t tick = 0;                // last use (LRU)
   void release() {
+    users.wait_all();
+    if (ready) (void)hipEventSynchronize(ready);
+    users.release();
     (void)hipFree(d_chroma);
-    d_chroma = nullptr;
-    chroma_built = false;
-    chroma_share = -1.0;
+    (void)hipHostFree(h_cost);
     (void)hipFree(d_tables);
     (void)hipHostFree(h_tables);
     (void)hipFree(d_stripe);
     (void)hipHostFree(h_stripe);
-    d_tables = nullptr; h_tables = nullptr; d_stripe = nullptr; h_stripe = nullptr;
-    groups_cap = 0;
+    if (ready) (void)hipEventDestroy(ready);
+    if (cost_ready) (void)hipEventDestroy(cost_ready);
+    *this = TableSet();
+  }
+  bool idle() const { return users.idle() && (!ready || hipEventQuery(ready) == hipSuccess); }
+  // the exact-path share, once the readback has landed (-1 before)
+  double share() {
+    if (chroma_share < 0 && chroma_built && hipEventQuery(cost_ready) == hipSuccess) {
+      double sh = 0.0;
+      for (int g = 0; g < groups_cap; ++g) {
+        const double v = (double)h_cost[g] / 4294967296.0;
+        if (v > sh) sh = v;
+      }
+      chroma_share = sh;
+    }
+    return chroma_share;
   }
 };
+constexpr int kTableSets = 4;
 
 struct TrikCvHandle {
   int device = 0;
@@ -168,17 +233,23 @@ struct TrikCvHandle {
   int out_w = 0, out_h = 0, out_ll = 0;
   std::mutex mu;
 
-  // compiled range tables (device) and the key they were compiled from
-  // two caches: the range set of the sums path, and a single range for the
-  // preview / multi-blob bitmap (so alternating calls do not recompile)
-  TableSet sums_tables, single_tables;
-  hipEvent_t tables_busy = nullptr;
+  // compiled range tables (device), LRU over the range sets in use
+  TableSet sets[kTableSets];
+  uint64_t tick = 0;
+  TableSet* sums_set = nullptr;  // the set of the last batched-sums call (trik_hsv_chroma_share)
+  // hot-kernel choice for this handle (trik_hsv_set_hot_kernel) and the kernel
+  // its last hot launch ran; pending_set: that launch let the device choose
+  // (the share was not known yet), resolved by trik_hsv_last_hot_kernel
+  std::atomic<int> hot{TRIK_HSV_HOT_AUTO};
+  int last_hot = 0;
+  TableSet* pending_set = nullptr;
 
   // preview geometry: scale maps for maps_key = {W, H, out_w, out_h}
   uint32_t* d_maps = nullptr;
   size_t d_maps_cap = 0;
   int maps_key[6] = {-1, -1, -1, -1, -1, -1};
   std::vector<uint32_t> h_maps;
+  StreamUses maps_users;
 
   // process() staging
   hipStream_t stream = nullptr;
@@ -201,7 +272,7 @@ struct TrikCvHandle {
   size_t d_blob_top_cap = 0;
   TrikHsvTarget* d_blob_targets = nullptr;
   size_t d_blob_targets_cap = 0;
-  hipEvent_t blob_busy = nullptr;
+  StreamUses blob_users;  // calls that wrote the multi-blob scratch
 };
 
 namespace {
@@ -212,22 +283,21 @@ void release(TrikCvHandle* h) {
   bool switched = hipGetDevice(&prev) == hipSuccess && prev != h->device &&
                   hipSetDevice(h->device) == hipSuccess;
   if (h->stream) (void)hipStreamSynchronize(h->stream);
-  if (h->tables_busy) (void)hipEventSynchronize(h->tables_busy);
-  h->sums_tables.release();
-  h->single_tables.release();
+  for (TableSet& t : h->sets) t.release();
+  h->maps_users.wait_all();
+  h->maps_users.release();
+  h->blob_users.wait_all();
+  h->blob_users.release();
   (void)hipFree(h->d_frame);
   (void)hipFree(h->d_maps);
   (void)hipFree(h->d_preview);
   (void)hipFree(h->d_auto);
   (void)hipFree(h->d_sums);
   (void)hipFree(h->d_targets);
-  if (h->blob_busy) (void)hipEventSynchronize(h->blob_busy);
   (void)hipFree(h->d_meta);
   (void)hipFree(h->d_blob_stats);
   (void)hipFree(h->d_blob_top);
   (void)hipFree(h->d_blob_targets);
-  if (h->blob_busy) (void)hipEventDestroy(h->blob_busy);
-  if (h->tables_busy) (void)hipEventDestroy(h->tables_busy);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   if (switched) (void)hipSetDevice(prev);
   delete h;
@@ -289,9 +359,13 @@ int32_t setup_dynamic(TrikCvHandle* h, const TRIK_VIDTRANSCODE_CV_DynamicParams*
   return setup_image_desc(h);
 }
 
-// Compile + upload the tables for ranges[0..n), stream-ordered on s.
-int32_t ensure_tables(TrikCvHandle* h, TableSet& t, const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n,
-                      hipStream_t s) {
+// The tables for ranges[0..n), stream-ordered on s: a cached set (s waits
+// for its uploads, device side), or a set compiled now into a slot whose
+// earlier uses have completed -- found without blocking (hipEventQuery);
+// only when all kTableSets sets are still in use does the host wait for the
+// least recently used one.
+int32_t acquire_tables(TrikCvHandle* h, const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, hipStream_t s,
+                       TableSet** out) {
   std::vector<uint32_t> key;
   key.reserve(3 * n + 1);
   key.push_back((uint32_t)n);
@@ -299,60 +373,106 @@ int32_t ensure_tables(TrikCvHandle* h, TableSet& t, const TRIK_VIDTRANSCODE_CV_I
     const PackedRange p = pack_range(ranges[i]);
     key.push_back(p.from); key.push_back(p.to); key.push_back(p.expect);
   }
-  if (key == t.key && t.d_tables) return 0;
-  const int groups = (n + kRangesPerLaunch - 1) / kRangesPerLaunch;
-  if (h->tables_busy) HIP_TRY(hipEventSynchronize(h->tables_busy));  // previous users done
-  if (groups > t.groups_cap) {
-    t.release();
-    HIP_TRY(hipMalloc(&t.d_tables, sizeof(RangeTables) * groups));
-    HIP_TRY(hipHostMalloc(&t.h_tables, sizeof(RangeTables) * groups, hipHostMallocDefault));
-    HIP_TRY(hipMalloc(&t.d_stripe, sizeof(StripeTables) * groups));
-    HIP_TRY(hipHostMalloc(&t.h_stripe, sizeof(StripeTables) * groups, hipHostMallocDefault));
-    t.groups_cap = groups;
+  for (TableSet& t : h->sets)
+    if (!t.key.empty() && t.key == key) {
+      if (t.ready) HIP_TRY(hipStreamWaitEvent(s, t.ready, 0));
+      t.tick = ++h->tick;
+      *out = &t;
+      return 0;
+    }
+  TableSet* v = nullptr;
+  for (TableSet& t : h->sets)
+    if (t.key.empty()) { v = &t; break; }
+  if (!v)
+    for (TableSet& t : h->sets)
+      if (t.idle() && (!v || t.tick < v->tick)) v = &t;
+  if (!v) {  // every set is in use: wait for the least recently used one
+    for (TableSet& t : h->sets)
+      if (!v || t.tick < v->tick) v = &t;
+    v->users.wait_all();
+    if (v->ready) HIP_TRY(hipEventSynchronize(v->ready));
   }
+  if (h->pending_set == v) h->pending_set = nullptr;
+  const int groups = (n + kRangesPerLaunch - 1) / kRangesPerLaunch;
+  if (groups > v->groups_cap) {
+    v->release();
+    HIP_TRY(hipMalloc(&v->d_tables, sizeof(RangeTables) * groups));
+    HIP_TRY(hipHostMalloc(&v->h_tables, sizeof(RangeTables) * groups, hipHostMallocDefault));
+    HIP_TRY(hipMalloc(&v->d_stripe, sizeof(StripeTables) * groups));
+    HIP_TRY(hipHostMalloc(&v->h_stripe, sizeof(StripeTables) * groups, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(&v->h_cost, sizeof(unsigned long long) * groups, hipHostMallocDefault));
+    HIP_TRY(hipEventCreateWithFlags(&v->ready, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&v->cost_ready, hipEventDisableTiming));
+    v->groups_cap = groups;
+  }
+  v->key.clear();  // invalid until the uploads are enqueued
+  // the set's earlier uploads and readers have finished (idle), so its pinned
+  // staging and device tables may be rewritten
   for (int g = 0; g < groups; ++g) {
     const int cnt = n - g * kRangesPerLaunch < kRangesPerLaunch ? n - g * kRangesPerLaunch : kRangesPerLaunch;
-    compile_tables(ranges + g * kRangesPerLaunch, cnt, &t.h_tables[g]);
-    compile_stripe_tables(t.h_tables[g], cnt, &t.h_stripe[g]);
+    compile_tables(ranges + g * kRangesPerLaunch, cnt, &v->h_tables[g]);
+    compile_stripe_tables(v->h_tables[g], cnt, &v->h_stripe[g]);
   }
-  HIP_TRY(hipMemcpyAsync(t.d_tables, t.h_tables, sizeof(RangeTables) * groups, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(t.d_stripe, t.h_stripe, sizeof(StripeTables) * groups, hipMemcpyHostToDevice, s));
-  t.key.swap(key);
-  t.chroma_built = false;
+  HIP_TRY(hipMemcpyAsync(v->d_tables, v->h_tables, sizeof(RangeTables) * groups, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(v->d_stripe, v->h_stripe, sizeof(StripeTables) * groups, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipEventRecord(v->ready, s));
+  v->key.swap(key);
+  v->chroma_built = false;
+  v->chroma_share = -1.0;
+  v->tick = ++h->tick;
+  *out = v;
   return 0;
 }
 
-// The chroma-run kernel's tables for the current range set (built on the
-// device from the uploaded RangeTables, stream-ordered on s).
-// Also reads back the builder's expected exact-path share (one small
-// synchronous copy per range set).
+// The chroma-run kernel's tables for the set's range groups, built on the
+// device from the uploaded RangeTables (stream-ordered on s).  The builder's
+// expected exact-path cost is copied back into pinned memory without waiting:
+// TableSet::share() reads it once it has landed.
 int32_t ensure_chroma(TableSet& t, int groups, hipStream_t s) {
   if (t.chroma_built) return 0;
   if (!t.d_chroma) HIP_TRY(hipMalloc(&t.d_chroma, sizeof(ChromaTables) * t.groups_cap));
-  double share = 0.0;
   for (int g = 0; g < groups; ++g) {
     HIP_TRY(build_chroma_tables(t.d_tables + g, t.d_chroma + g, s));
-    unsigned long long cost = 0;
-    HIP_TRY(hipMemcpyAsync(&cost, &t.d_chroma[g].flagged_cost, sizeof(cost), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    const double sh = (double)cost / 4294967296.0;
-    if (sh > share) share = sh;
+    HIP_TRY(hipMemcpyAsync(&t.h_cost[g], &t.d_chroma[g].flagged_cost, sizeof(unsigned long long),
+                           hipMemcpyDeviceToHost, s));
   }
-  t.chroma_share = share;
+  for (int g = groups; g < t.groups_cap; ++g) t.h_cost[g] = 0;
+  HIP_TRY(hipEventRecord(t.cost_ready, s));
+  HIP_TRY(hipEventRecord(t.ready, s));  // later users on other streams wait for the build too
   t.chroma_built = true;
+  t.chroma_share = -1.0;
   return 0;
 }
 
-std::atomic<int> g_hot_kernel{TRIK_HSV_HOT_AUTO};
-thread_local int g_last_hot = 0;
+// How the hot kernel is chosen for one launch: CHROMA / STRIPE decided on the
+// host, or GATED: both launched, the device picks by the builder's cost.
+enum HotPlan { kPlanStripe, kPlanChroma, kPlanGated };
+
+HotPlan plan_hot(TrikCvHandle* h, TableSet& t, int groups, bool big, bool chroma_ok, hipStream_t s,
+                 int32_t* rc) {
+  *rc = 0;
+  const int choice = h->hot.load();
+  if (!chroma_ok || !(choice == TRIK_HSV_HOT_CHROMA || (choice == TRIK_HSV_HOT_AUTO && big))) return kPlanStripe;
+  *rc = ensure_chroma(t, groups, s);
+  if (*rc) return kPlanStripe;
+  if (choice == TRIK_HSV_HOT_CHROMA) return kPlanChroma;
+  const double sh = t.share();
+  if (sh < 0) return kPlanGated;  // the share is still in flight: no host wait
+  return sh <= TRIK_HSV_CHROMA_MAX_SHARE ? kPlanChroma : kPlanStripe;
+}
 
 int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
                  const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, TrikHsvTargetSums* sums,
                  uint8_t* masks, hipStream_t s) {
-  int32_t rc = ensure_tables(h, h->sums_tables, ranges, n, s);
+  TableSet* t = nullptr;
+  int32_t rc = acquire_tables(h, ranges, n, s, &t);
   if (rc) return rc;
+  h->sums_set = t;
   if (b->n_frames == 0 || b->width == 0 || b->height == 0) return 0;
-  for (int g = 0; g * kRangesPerLaunch < n; ++g) {
+  const int groups = (n + kRangesPerLaunch - 1) / kRangesPerLaunch;
+  const bool big = (int64_t)b->n_frames * b->width * b->height >= (int64_t)TRIK_HSV_CHROMA_MIN_PIXELS;
+  bool gated = false;
+  for (int g = 0; g < groups; ++g) {
     KernelArgs a;
     a.frames = static_cast<const uint8_t*>(b->frames);
     a.frame_stride = b->n_frames > 1 ? b->frame_stride : 0;
@@ -362,51 +482,60 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
     a.n_ranges = n - g * kRangesPerLaunch < kRangesPerLaunch ? n - g * kRangesPerLaunch : kRangesPerLaunch;
     a.range_offset = g * kRangesPerLaunch;
     a.sums_ranges = n;
-    a.tables = h->sums_tables.d_tables + g;
-    a.stripe_tables = h->sums_tables.d_stripe + g;
+    a.tables = t->d_tables + g;
+    a.stripe_tables = t->d_stripe + g;
     a.sums = sums;
     a.masks = masks;
     a.mask_shift = g * kRangesPerLaunch;
     // the chroma-run kernel for large batches, the stripe kernel otherwise;
     // the generic kernel takes misaligned inputs and rows wider than 8192 pixels
-    const int choice = g_hot_kernel.load();
-    const bool big = (int64_t)b->n_frames * b->width * b->height >= (int64_t)TRIK_HSV_CHROMA_MIN_PIXELS;
+    const HotPlan plan = plan_hot(h, *t, groups, big, h->hot.load() != TRIK_HSV_HOT_GENERIC && chroma_geometry_ok(a),
+                                  s, &rc);
+    if (rc) return rc;
     int e = hipErrorNotSupported;
-    if ((choice == TRIK_HSV_HOT_CHROMA || (choice == TRIK_HSV_HOT_AUTO && big)) && chroma_geometry_ok(a)) {
-      HIP_TRY(ensure_chroma(h->sums_tables, (n + kRangesPerLaunch - 1) / kRangesPerLaunch, s));
-      // AUTO keeps range sets whose profiles send too much to the exact path
-      // (many separate runs per chroma) on the stripe kernel
-      if (choice == TRIK_HSV_HOT_CHROMA || h->sums_tables.chroma_share <= TRIK_HSV_CHROMA_MAX_SHARE) {
-        e = launch_chroma(a, h->sums_tables.d_chroma + g, masks != nullptr, s);
-        if (e == hipSuccess) g_last_hot = TRIK_HSV_HOT_CHROMA;
-      }
+    if (plan == kPlanChroma) {
+      e = launch_chroma(a, t->d_chroma + g, masks != nullptr, s);
+      if (e == hipSuccess) h->last_hot = TRIK_HSV_HOT_CHROMA;
+    } else if (plan == kPlanGated) {
+      // AUTO's rule on the device: the chroma-run kernel runs while this
+      // group's cost is at most kChromaMaxCost, the stripe kernel otherwise
+      KernelArgs ac = a, as = a;
+      ac.gate = as.gate = &t->d_chroma[g].flagged_cost;
+      ac.gate_max = as.gate_max = kChromaMaxCost;
+      ac.gate_le = 1;
+      as.gate_le = 0;
+      e = launch_chroma(ac, t->d_chroma + g, masks != nullptr, s);
+      if (e == hipSuccess) e = launch_stripe(as, masks != nullptr, s);
+      if (e == hipSuccess) gated = true;
     }
-    if (e == hipErrorNotSupported && choice != TRIK_HSV_HOT_GENERIC) {
+    if (e == hipErrorNotSupported && h->hot.load() != TRIK_HSV_HOT_GENERIC) {
       e = launch_stripe(a, masks != nullptr, s);
-      if (e == hipSuccess) g_last_hot = TRIK_HSV_HOT_STRIPE;
+      if (e == hipSuccess) h->last_hot = TRIK_HSV_HOT_STRIPE;
     }
     if (e == hipErrorNotSupported) {
       e = launch_reduce(a, masks != nullptr, s);
-      if (e == hipSuccess) g_last_hot = TRIK_HSV_HOT_GENERIC;
+      if (e == hipSuccess) h->last_hot = TRIK_HSV_HOT_GENERIC;
     }
     HIP_TRY(e);
   }
-  if (!h->tables_busy) HIP_TRY(hipEventCreateWithFlags(&h->tables_busy, hipEventDisableTiming));
-  HIP_TRY(hipEventRecord(h->tables_busy, s));
-  return 0;
+  h->pending_set = gated ? t : nullptr;
+  rc = t->users.note(s);
+  return rc ? fail(TRIK_IVIDTRANSCODE_EFAIL, std::string("hipEventRecord: ") + hipGetErrorString((hipError_t)rc)) : 0;
 }
 
 inline void set_bit(int32_t& word, int bit) { word |= (int32_t)(1u << bit); }
 
 // Scale maps of the preview (WSEQ:371-387) for this geometry, uploaded once.
 // col_lo..col_hi: the source columns that write (the line sensor's window).
+// A geometry change (rare) waits for the kernels still reading the old maps
+// and for the upload (the staging is pageable and reused).
 int32_t ensure_maps(TrikCvHandle* h, int w, int hgt, int ow, int oh, hipStream_t s, int col_lo = 0,
                     int col_hi = 0x7FFFFFFF) {
   if (h->d_maps && h->maps_key[0] == w && h->maps_key[1] == hgt && h->maps_key[2] == ow &&
       h->maps_key[3] == oh && h->maps_key[4] == col_lo && h->maps_key[5] == col_hi)
     return 0;
   const size_t n = (size_t)w + hgt + ow + oh;
-  if (h->tables_busy) HIP_TRY(hipEventSynchronize(h->tables_busy));  // previous users done
+  h->maps_users.wait_all();  // previous users done
   if (n > h->d_maps_cap) {
     (void)hipFree(h->d_maps);
     h->d_maps = nullptr; h->d_maps_cap = 0;
@@ -445,14 +574,21 @@ PreviewArgs preview_args(const TrikCvHandle* h, const TrikHsvFrameBatch& b,
   return a;
 }
 
-// The preview's detection range compiled into the single-range tables.
+// The preview's detection range compiled as a single-range table set.
 int32_t preview_tables(TrikCvHandle* h, PreviewArgs& pa, const TRIK_VIDTRANSCODE_CV_InArgsAlg& range,
-                       hipStream_t s) {
-  int32_t rc = ensure_tables(h, h->single_tables, &range, 1, s);
+                       hipStream_t s, TableSet** set) {
+  int32_t rc = acquire_tables(h, &range, 1, s, set);
   if (rc) return rc;
   pa.range = pack_range(range);
-  pa.tables = h->single_tables.d_stripe;
+  pa.tables = (*set)->d_stripe;
   return 0;
+}
+
+// Record that the work just enqueued on s reads `set` (and the preview maps).
+int32_t note_uses(TrikCvHandle* h, TableSet* set, bool maps, hipStream_t s) {
+  int32_t r = set ? set->users.note(s) : 0;
+  if (!r && maps) r = h->maps_users.note(s);
+  return r ? fail(TRIK_IVIDTRANSCODE_EFAIL, std::string("hipEventRecord: ") + hipGetErrorString((hipError_t)r)) : 0;
 }
 
 // The line sensor's range in the object sensor's terms: hue 0..359 and
@@ -527,11 +663,16 @@ int32_t grow(T*& p, size_t& cap, size_t bytes) {
   return 0;
 }
 
-// Scratch for n frames of W x H; waits for the previous blob work of the handle.
-int32_t ensure_blob_scratch(TrikCvHandle* h, int n, int w, int hgt) {
-  if (h->blob_busy) HIP_TRY(hipEventSynchronize(h->blob_busy));
+// Scratch for n frames of W x H.  Stream s waits (device side) for the
+// handle's earlier multi-blob work on other streams, which used the same
+// scratch; growing it (a larger batch) waits for that work on the host.
+int32_t ensure_blob_scratch(TrikCvHandle* h, int n, int w, int hgt, hipStream_t s) {
   const size_t bw = (size_t)(w / 4), bh = (size_t)(hgt / 4), nn = (size_t)(n > 0 ? n : 1);
   const size_t ml = (size_t)blob_max_labels((int)bw, (int)bh);
+  if (nn * (bw * bh > 0 ? bw * bh : 1) > h->d_meta_cap || nn * 6 * ml * sizeof(int32_t) > h->d_blob_stats_cap ||
+      nn * 24 * sizeof(int32_t) > h->d_blob_top_cap || nn * 8 * sizeof(TrikHsvTarget) > h->d_blob_targets_cap)
+    h->blob_users.wait_all();
+  HIP_TRY(h->blob_users.order_after(s));
   int32_t r = grow(h->d_meta, h->d_meta_cap, nn * (bw * bh > 0 ? bw * bh : 1));
   if (!r) r = grow(h->d_blob_stats, h->d_blob_stats_cap, nn * 6 * ml * sizeof(int32_t));
   if (!r) r = grow(h->d_blob_top, h->d_blob_top_cap, nn * 24 * sizeof(int32_t));
@@ -542,15 +683,15 @@ int32_t ensure_blob_scratch(TrikCvHandle* h, int n, int w, int hgt) {
 // Compiles the range's tables (cached per handle) and fills the kernel args.
 int32_t blob_args(TrikCvHandle* h, const TrikHsvFrameBatch& b, const TRIK_VIDTRANSCODE_CV_InArgsAlg& range,
                   TrikHsvTarget* targets, int32_t* top, uint8_t* meta, uint16_t* labels, int32_t* n_labels,
-                  hipStream_t s, BlobArgs& a) {
-  int32_t rc = ensure_tables(h, h->single_tables, &range, 1, s);
+                  hipStream_t s, BlobArgs& a, TableSet** set) {
+  int32_t rc = acquire_tables(h, &range, 1, s, set);
   if (rc) return rc;
   a.frames = static_cast<const uint8_t*>(b.frames);
   a.frame_stride = b.frame_stride;
   a.n_frames = b.n_frames;
   a.width = b.width; a.height = b.height; a.line_length = b.line_length;
   a.range = pack_range(range);
-  a.tables = h->single_tables.d_stripe;
+  a.tables = (*set)->d_stripe;
   a.aligned4 = (reinterpret_cast<uintptr_t>(b.frames) & 3) == 0 && (b.n_frames <= 1 || (b.frame_stride & 3) == 0) &&
                (b.line_length & 3) == 0;
   a.meta = meta ? meta : h->d_meta;
@@ -567,18 +708,27 @@ int32_t blob_args(TrikCvHandle* h, const TrikHsvFrameBatch& b, const TRIK_VIDTRA
 // sticky range when the hot-kernel setting allows it (AUTO: batches of at
 // least TRIK_HSV_CHROMA_MIN_PIXELS whose exact-path share is low), else the
 // stripe-arithmetic kernel inside launch_blob; then the clusterer.
-int32_t run_blob(TrikCvHandle* h, BlobArgs& ba, hipStream_t s) {
-  const int choice = g_hot_kernel.load();
+int32_t run_blob(TrikCvHandle* h, BlobArgs& ba, TableSet& t, hipStream_t s) {
   const bool big = (int64_t)ba.n_frames * ba.width * ba.height >= (int64_t)TRIK_HSV_CHROMA_MIN_PIXELS;
+  int32_t rc = 0;
+  const HotPlan plan = plan_hot(h, t, 1, big, h->hot.load() != TRIK_HSV_HOT_GENERIC && blob_chroma_ok(ba), s, &rc);
+  if (rc) return rc;
   ba.meta_ready = 0;
-  g_last_hot = TRIK_HSV_HOT_STRIPE;
-  if ((choice == TRIK_HSV_HOT_CHROMA || (choice == TRIK_HSV_HOT_AUTO && big)) && blob_chroma_ok(ba)) {
-    HIP_TRY(ensure_chroma(h->single_tables, 1, s));
-    if (choice == TRIK_HSV_HOT_CHROMA || h->single_tables.chroma_share <= TRIK_HSV_CHROMA_MAX_SHARE) {
-      HIP_TRY(launch_blob_meta_chroma(ba, h->single_tables.d_chroma, h->single_tables.d_tables, s));
-      ba.meta_ready = 1;
-      g_last_hot = TRIK_HSV_HOT_CHROMA;
-    }
+  h->pending_set = nullptr;
+  if (plan == kPlanChroma) {
+    HIP_TRY(launch_blob_meta_chroma(ba, t.d_chroma, t.d_tables, s));
+    ba.meta_ready = 1;
+    h->last_hot = TRIK_HSV_HOT_CHROMA;
+  } else if (plan == kPlanGated) {  // both bitmap kernels, the device runs one (see run_sums)
+    BlobArgs bc = ba;
+    bc.gate = ba.gate = &t.d_chroma[0].flagged_cost;
+    bc.gate_max = ba.gate_max = kChromaMaxCost;
+    bc.gate_le = 1;
+    ba.gate_le = 0;
+    HIP_TRY(launch_blob_meta_chroma(bc, t.d_chroma, t.d_tables, s));
+    h->pending_set = &t;
+  } else {
+    h->last_hot = TRIK_HSV_HOT_STRIPE;
   }
   HIP_TRY(launch_blob(ba, s));
   return 0;
@@ -781,12 +931,16 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
         HIP_TRY(hipMemsetAsync(h->d_sums, 0, sizeof(TrikHsvTargetSums), h->stream));
         if (blob) {  // BallDetector<YUV422P>::run, OSEQ:516-602
           if (ia7->alg.setHsvRange) h->blob_range = blob_range_args(ia7->alg);  // BMB:110-130
-          int32_t r = ensure_blob_scratch(h, 1, h->in_w, h->in_h);
+          int32_t r = ensure_blob_scratch(h, 1, h->in_w, h->in_h, h->stream);
           if (r) return r;
           BlobArgs ba;
-          r = blob_args(h, b, h->blob_range, nullptr, nullptr, nullptr, nullptr, nullptr, h->stream, ba);
+          TableSet* set = nullptr;
+          r = blob_args(h, b, h->blob_range, nullptr, nullptr, nullptr, nullptr, nullptr, h->stream, ba, &set);
           if (r) return r;
-          r = run_blob(h, ba, h->stream);
+          r = run_blob(h, ba, *set, h->stream);
+          if (r) return r;
+          r = note_uses(h, set, false, h->stream);
+          if (!r) r = h->blob_users.note(h->stream);
           if (r) return r;
           if (out_ptr && out_size > 0) {  // preview: set metapixels, guide lines, target marks
             const size_t pb = (size_t)out_size;
@@ -800,6 +954,8 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
             pa.meta = ba.meta;
             HIP_TRY(launch_preview_body(pa, h->stream));
             HIP_TRY(launch_blob_overlay(pa, ba.top, h->stream));
+            r = note_uses(h, nullptr, true, h->stream);
+            if (r) return r;
             HIP_TRY(hipMemcpyAsync(out_ptr, h->d_preview, pb, hipMemcpyDeviceToHost, h->stream));
           }
           TrikHsvTarget t[8];
@@ -829,10 +985,13 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
             int32_t r = ensure_maps(h, h->in_w, h->in_h, h->out_w, h->out_h, h->stream, 5, h->in_w - 5);
             if (r) return r;
             PreviewArgs pa = preview_args(h, b, ia, h->out_w, h->out_h, h->out_ll, h->d_preview, (int64_t)pb);
-            r = preview_tables(h, pa, line_alg(ia.detectValFrom, ia.detectValTo), h->stream);
+            TableSet* set = nullptr;
+            r = preview_tables(h, pa, line_alg(ia.detectValFrom, ia.detectValTo), h->stream, &set);
             if (r) return r;
             HIP_TRY(launch_preview_body(pa, h->stream));
             HIP_TRY(launch_line_overlay(pa, h->d_sums, h->stream));
+            r = note_uses(h, set, true, h->stream);
+            if (r) return r;
             HIP_TRY(hipMemcpyAsync(out_ptr, h->d_preview, pb, hipMemcpyDeviceToHost, h->stream));
           }
           TrikHsvTarget t;
@@ -868,9 +1027,12 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
           if (r) return r;
           PreviewArgs pa = preview_args(h, b, in_args->alg, h->out_w, h->out_h, h->out_ll, h->d_preview,
                                         (int64_t)pb);
-          r = preview_tables(h, pa, in_args->alg, h->stream);
+          TableSet* set = nullptr;
+          r = preview_tables(h, pa, in_args->alg, h->stream, &set);
           if (r) return r;
           HIP_TRY(launch_preview(pa, h->d_sums, 1, h->stream));
+          r = note_uses(h, set, true, h->stream);
+          if (r) return r;
           HIP_TRY(hipMemcpyAsync(out_ptr, h->d_preview, pb, hipMemcpyDeviceToHost, h->stream));
         }
         TrikHsvTarget t;
@@ -910,23 +1072,83 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
 // ---------------------------------------------------------------------------
 // Layer 2: batched device API
 // ---------------------------------------------------------------------------
-extern "C" int32_t trik_hsv_set_hot_kernel(int32_t kind) {
-  if (kind < TRIK_HSV_HOT_AUTO || kind > TRIK_HSV_HOT_GENERIC) return -1;
-  return g_hot_kernel.exchange(kind);
+namespace {
+
+// A batched call runs on the handle's device (one thread may drive several
+// GPUs, one handle each); the caller's current device is restored after.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    int cur = 0;
+    if (hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess) prev = cur;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// A device buffer handed to a batched call must be device-accessible memory
+// of the handle's device ("" if so).
+std::string device_buffer_error(const void* p, int dev, const char* what) {
+  if (!p) return "";
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return std::string(what) + " is not device-accessible memory";
+  }
+  if (at.type == hipMemoryTypeUnregistered)
+    return std::string(what) + " is pageable host memory, not device-accessible memory";
+  if (at.type == hipMemoryTypeDevice && at.device != dev)
+    return std::string(what) + " is on device " + std::to_string(at.device) + ", the handle on device " +
+           std::to_string(dev);
+  return "";
 }
 
-extern "C" int32_t trik_hsv_last_hot_kernel(void) { return g_last_hot; }
+}  // namespace
+
+extern "C" int32_t trik_hsv_set_hot_kernel(TRIK_VIDTRANSCODE_CV_Handle h, int32_t kind) {
+  if (!h || kind < TRIK_HSV_HOT_AUTO || kind > TRIK_HSV_HOT_GENERIC) return -1;
+  return h->hot.exchange(kind);
+}
+
+extern "C" int32_t trik_hsv_last_hot_kernel(TRIK_VIDTRANSCODE_CV_Handle h) {
+  if (!h) return 0;
+  std::lock_guard<std::mutex> lock(h->mu);
+  if (h->pending_set) {  // the device chose: resolve it from the builder's cost
+    DeviceGuard dg(h->device);
+    TableSet* t = h->pending_set;
+    (void)hipEventSynchronize(t->cost_ready);
+    h->last_hot = t->share() <= TRIK_HSV_CHROMA_MAX_SHARE ? TRIK_HSV_HOT_CHROMA : TRIK_HSV_HOT_STRIPE;
+    h->pending_set = nullptr;
+  }
+  return h->last_hot;
+}
 
 extern "C" int32_t trik_hsv_chroma_share(TRIK_VIDTRANSCODE_CV_Handle h, double* share) {
   if (!h || !share) return fail(TRIK_IVIDTRANSCODE_EFAIL, "NULL handle or share");
   std::lock_guard<std::mutex> lock(h->mu);
-  *share = h->sums_tables.chroma_built ? h->sums_tables.chroma_share : -1.0;
+  DeviceGuard dg(h->device);
+  TableSet* t = h->sums_set;
+  *share = -1.0;
+  if (t && t->chroma_built) {
+    HIP_TRY(hipEventSynchronize(t->cost_ready));
+    *share = t->share();
+  }
   return 0;
 }
 
 extern "C" const char* trik_hsv_version(void) { return "trik-hsv-mi355x 0.1.0 (gfx950)"; }
 
 extern "C" const char* trik_hsv_last_error(void) { return g_last_error.c_str(); }
+
+// The batch's frames and the output buffer live on the handle's device.
+static int32_t check_device(TRIK_VIDTRANSCODE_CV_Handle h, const TrikHsvFrameBatch* b, const void* out) {
+  if (!b || b->n_frames <= 0) return 0;
+  DeviceGuard dg(h->device);
+  std::string e = device_buffer_error(b->frames, h->device, "frames");
+  if (e.empty()) e = device_buffer_error(out, h->device, "the output buffer");
+  return e.empty() ? 0 : fail(TRIK_IVIDTRANSCODE_EFAIL, e);
+}
 
 static int32_t check_common(TRIK_VIDTRANSCODE_CV_Handle h, const TrikHsvFrameBatch* b,
                             const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int32_t n,
@@ -937,7 +1159,7 @@ static int32_t check_common(TRIK_VIDTRANSCODE_CV_Handle h, const TrikHsvFrameBat
   if (n < 1 || n > TRIK_HSV_MAX_RANGES || !ranges)
     return fail(TRIK_IVIDTRANSCODE_EFAIL, "n_ranges must be 1..64");
   if (!sums && b->n_frames > 0) return fail(TRIK_IVIDTRANSCODE_EFAIL, "sums is NULL");
-  return 0;
+  return check_device(h, b, sums);
 }
 
 extern "C" int32_t trik_hsv_batch_sums(TRIK_VIDTRANSCODE_CV_Handle h, const TrikHsvFrameBatch* b,
@@ -946,6 +1168,7 @@ extern "C" int32_t trik_hsv_batch_sums(TRIK_VIDTRANSCODE_CV_Handle h, const Trik
   int32_t rc = check_common(h, b, ranges, n, sums);
   if (rc) return rc;
   std::lock_guard<std::mutex> lock(h->mu);
+  DeviceGuard dg(h->device);
   return run_sums(h, b, ranges, n, sums, nullptr, static_cast<hipStream_t>(stream));
 }
 
@@ -970,6 +1193,7 @@ extern "C" int32_t trik_hsv_process_batch(TRIK_VIDTRANSCODE_CV_Handle h, const T
   if (rc) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   std::lock_guard<std::mutex> lock(h->mu);
+  DeviceGuard dg(h->device);
   if (b->n_frames > 0)
     HIP_TRY(hipMemsetAsync(sums, 0, sizeof(TrikHsvTargetSums) * (size_t)b->n_frames * n, s));
   rc = run_sums(h, b, ranges, n, sums, nullptr, s);
@@ -986,6 +1210,7 @@ extern "C" int32_t trik_hsv_batch_masks(TRIK_VIDTRANSCODE_CV_Handle h, const Tri
   if (n > 8) return fail(TRIK_IVIDTRANSCODE_EFAIL, "mask mode supports at most 8 ranges");
   if (!masks && b->n_frames > 0) return fail(TRIK_IVIDTRANSCODE_EFAIL, "masks is NULL");
   std::lock_guard<std::mutex> lock(h->mu);
+  DeviceGuard dg(h->device);
   return run_sums(h, b, ranges, n, sums, masks, static_cast<hipStream_t>(stream));
 }
 
@@ -1005,17 +1230,19 @@ extern "C" int32_t trik_hsv_batch_preview(TRIK_VIDTRANSCODE_CV_Handle h, const T
   if (!previews && b->n_frames > 0 && pb > 0) return fail(TRIK_IVIDTRANSCODE_EFAIL, "previews is NULL");
   hipStream_t s = static_cast<hipStream_t>(stream);
   std::lock_guard<std::mutex> lock(h->mu);
+  DeviceGuard dg(h->device);
   if (b->n_frames == 0 || pb == 0) return 0;
+  rc = check_device(h, b, previews);
+  if (rc) return rc;
   // the preview kernel writes every byte of each preview, zeros included (WFXNS:234)
   rc = ensure_maps(h, b->width, b->height, out_width, out_height, s);
   if (rc) return rc;
   PreviewArgs pa = preview_args(h, *b, *range, out_width, out_height, out_line_length, previews, preview_stride);
-  rc = preview_tables(h, pa, *range, s);
+  TableSet* set = nullptr;
+  rc = preview_tables(h, pa, *range, s, &set);
   if (rc) return rc;
   HIP_TRY(launch_preview(pa, sums, sums_pitch, s));
-  if (!h->tables_busy) HIP_TRY(hipEventCreateWithFlags(&h->tables_busy, hipEventDisableTiming));
-  HIP_TRY(hipEventRecord(h->tables_busy, s));
-  return 0;
+  return note_uses(h, set, true, s);
 }
 
 extern "C" int32_t trik_hsv_batch_auto_range(const TrikHsvFrameBatch* b, uint16_t* out, void* stream) {
@@ -1062,19 +1289,21 @@ extern "C" int32_t trik_hsv_line_preview(TRIK_VIDTRANSCODE_CV_Handle h, const Tr
   if (b->n_frames > 0 && pb > 0 && (!previews || !sums)) return fail(TRIK_IVIDTRANSCODE_EFAIL, "NULL buffer");
   hipStream_t s = static_cast<hipStream_t>(stream);
   std::lock_guard<std::mutex> lock(h->mu);
+  DeviceGuard dg(h->device);
   if (b->n_frames == 0 || pb == 0) return 0;
-  int32_t rc = ensure_maps(h, b->width, b->height, out_width, out_height, s, 5, b->width - 5);
+  int32_t rc = check_device(h, b, previews);
+  if (rc) return rc;
+  rc = ensure_maps(h, b->width, b->height, out_width, out_height, s, 5, b->width - 5);
   if (rc) return rc;
   TRIK_VIDTRANSCODE_CV_InArgsAlg ia;
   memset(&ia, 0, sizeof ia);
   PreviewArgs pa = preview_args(h, *b, ia, out_width, out_height, out_line_length, previews, preview_stride);
-  rc = preview_tables(h, pa, line_alg(val_from, val_to), s);
+  TableSet* set = nullptr;
+  rc = preview_tables(h, pa, line_alg(val_from, val_to), s, &set);
   if (rc) return rc;
   HIP_TRY(launch_preview_body(pa, s));
   HIP_TRY(launch_line_overlay(pa, sums, s));
-  if (!h->tables_busy) HIP_TRY(hipEventCreateWithFlags(&h->tables_busy, hipEventDisableTiming));
-  HIP_TRY(hipEventRecord(h->tables_busy, s));
-  return 0;
+  return note_uses(h, set, true, s);
 }
 
 extern "C" int32_t trik_hsv_blob_batch(TRIK_VIDTRANSCODE_CV_Handle h, const TrikHsvFrameBatch* b,
@@ -1093,25 +1322,27 @@ extern "C" int32_t trik_hsv_blob_batch(TRIK_VIDTRANSCODE_CV_Handle h, const Trik
   if (b->n_frames > 0 && !targets) return fail(TRIK_IVIDTRANSCODE_EFAIL, "targets is NULL");
   hipStream_t s = static_cast<hipStream_t>(stream);
   std::lock_guard<std::mutex> lock(h->mu);
+  DeviceGuard dg(h->device);
   if (b->n_frames == 0) return 0;
+  int32_t r = check_device(h, b, targets);
+  if (r) return r;
   if (b->width == 0 || b->height == 0) {
     HIP_TRY(hipMemsetAsync(targets, 0, sizeof(TrikHsvTarget) * 8 * (size_t)b->n_frames, s));
     if (top) HIP_TRY(hipMemsetAsync(top, 0, sizeof(int32_t) * 24 * (size_t)b->n_frames, s));
     if (n_labels) HIP_TRY(hipMemsetAsync(n_labels, 0, sizeof(int32_t) * (size_t)b->n_frames, s));
     return 0;
   }
-  int32_t r = ensure_blob_scratch(h, b->n_frames, b->width, b->height);
+  r = ensure_blob_scratch(h, b->n_frames, b->width, b->height, s);
   if (r) return r;
   BlobArgs ba;
-  r = blob_args(h, *b, blob_range_args(*hsv), targets, top, meta, labels, n_labels, s, ba);
+  TableSet* set = nullptr;
+  r = blob_args(h, *b, blob_range_args(*hsv), targets, top, meta, labels, n_labels, s, ba, &set);
   if (r) return r;
-  r = run_blob(h, ba, s);
+  r = run_blob(h, ba, *set, s);
   if (r) return r;
-  if (!h->tables_busy) HIP_TRY(hipEventCreateWithFlags(&h->tables_busy, hipEventDisableTiming));
-  HIP_TRY(hipEventRecord(h->tables_busy, s));
-  if (!h->blob_busy) HIP_TRY(hipEventCreateWithFlags(&h->blob_busy, hipEventDisableTiming));
-  HIP_TRY(hipEventRecord(h->blob_busy, s));
-  return 0;
+  r = note_uses(h, set, false, s);
+  if (!r) r = h->blob_users.note(s);
+  return r ? fail(TRIK_IVIDTRANSCODE_EFAIL, "hipEventRecord failed") : 0;
 }
 
 extern "C" int32_t trik_hsv_blob_preview(TRIK_VIDTRANSCODE_CV_Handle h, const TrikHsvFrameBatch* b,
@@ -1131,8 +1362,11 @@ extern "C" int32_t trik_hsv_blob_preview(TRIK_VIDTRANSCODE_CV_Handle h, const Tr
   if (b->n_frames > 0 && pb > 0 && (!previews || !meta || !top)) return fail(TRIK_IVIDTRANSCODE_EFAIL, "NULL buffer");
   hipStream_t s = static_cast<hipStream_t>(stream);
   std::lock_guard<std::mutex> lock(h->mu);
+  DeviceGuard dg(h->device);
   if (b->n_frames == 0 || pb == 0) return 0;
-  int32_t rc = ensure_maps(h, b->width, b->height, out_width, out_height, s);
+  int32_t rc = check_device(h, b, previews);
+  if (rc) return rc;
+  rc = ensure_maps(h, b->width, b->height, out_width, out_height, s);
   if (rc) return rc;
   TRIK_VIDTRANSCODE_CV_InArgsAlg none;
   memset(&none, 0, sizeof none);
@@ -1140,9 +1374,7 @@ extern "C" int32_t trik_hsv_blob_preview(TRIK_VIDTRANSCODE_CV_Handle h, const Tr
   pa.meta = meta;
   HIP_TRY(launch_preview_body(pa, s));
   HIP_TRY(launch_blob_overlay(pa, top, s));
-  if (!h->tables_busy) HIP_TRY(hipEventCreateWithFlags(&h->tables_busy, hipEventDisableTiming));
-  HIP_TRY(hipEventRecord(h->tables_busy, s));
-  return 0;
+  return note_uses(h, nullptr, true, s);
 }
 
 extern "C" int32_t trik_hsv_synth(const TrikHsvFrameBatch* b, int32_t first_frame, int32_t kind,

@@ -54,6 +54,7 @@ struct MetaGeom {
 // metapixels of the batch; two workgroups per CU as stripe_kernel.
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8)))
 void blob_meta_kernel(BlobArgs a, MetaGeom g) {
+  if (gated_out(a.gate, a.gate_max, a.gate_le)) return;
   {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     const u32x4* src = reinterpret_cast<const u32x4*>(a.tables);
@@ -439,20 +440,11 @@ int launch_blob(const BlobArgs& a, hipStream_t s) {
   if (z != hipSuccess) return z;
   const int64_t total = (int64_t)a.n_frames * bw * bh;
   if (total >= (1ll << 31) || !a.tables) return hipErrorInvalidValue;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(blob_meta_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(StripeTables));
+  {
+    hipError_t e = set_dynamic_lds(reinterpret_cast<const void*>(blob_meta_kernel), (int)sizeof(StripeTables));
     if (e != hipSuccess) return e;
-    attr = true;
   }
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-  }
+  const int cus = device_cus();
   if (total > 0 && !a.meta_ready) {
     MetaGeom g;
     g.per_frame = make_div((uint32_t)(bw * bh));

@@ -421,6 +421,7 @@ struct ExcSums {
 
 template <int LAYOUT, int NR, bool MASKS, int CW>
 __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaGeom g, const ChromaTables* ct) {
+  if (gated_out(a.gate, a.gate_max, a.gate_le)) return;
   const int t = threadIdx.x;
   {  // stage block masks, the mask-pair table and the run descriptors
     for (int i = t; i < 8192 / 16; i += blockDim.x)
@@ -455,7 +456,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
   const int col_bytes = LAYOUT == TRIK_HSV_LAYOUT_YUYV ? col * 16 : col * 2 * CW;
   const uint32_t x0 = (uint32_t)col * (SPLIT ? 8u : 2u * CW);
   const uint32_t voff = (uint32_t)ro * (uint32_t)a.line_length + (uint32_t)col_bytes;
-  auto xoff = [dx](int i) { return SPLIT ? (i < 4 ? 0u : dx) + 2u * (uint32_t)(i & 3) : 2u * (uint32_t)i; };
+  auto xoff = [=](int i) { return SPLIT ? (i < 4 ? 0u : dx) + 2u * (uint32_t)(i & 3) : 2u * (uint32_t)i; };
 
   const int64_t t_begin = g.n_tiles * blockIdx.x / gridDim.x;
   const int64_t t_end = g.n_tiles * (blockIdx.x + 1) / gridDim.x;
@@ -731,6 +732,7 @@ struct BlobChromaGeom {
 __global__ __launch_bounds__(kMaxBlock) void blob_chroma_meta_kernel(BlobArgs a, BlobChromaGeom g,
                                                                       const ChromaTables* ct,
                                                                       const RangeTables* rt) {
+  if (gated_out(a.gate, a.gate_max, a.gate_le)) return;
   const int t = threadIdx.x;
   {  // the chroma kernel's tables (one range), zeroed count words
     for (int i = t; i < 8192 / 16; i += blockDim.x)
@@ -839,26 +841,12 @@ __global__ __launch_bounds__(kMaxBlock) void blob_chroma_meta_kernel(BlobArgs a,
   }
 }
 
-int cu_count() {
-  int dev = 0, n = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 256;
-  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-    return 256;
-  return n;
-}
-
 template <int LAYOUT, int NR, bool MASKS>
 int launch_t(const KernelArgs& a, const ChromaGeom& g, const ChromaTables* ct, hipStream_t s) {
   auto kern = chroma_kernel<LAYOUT, NR, MASKS, kChunkWords>;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  static int cus = 0;
-  if (!cus) cus = cu_count();
+  hipError_t e = set_dynamic_lds(reinterpret_cast<const void*>(kern), (int)kLdsBytes);
+  if (e != hipSuccess) return e;
+  const int cus = device_cus();
   const int block = ((g.k * g.cpr + 63) / 64) * 64;
   const int64_t grid = g.n_tiles < cus ? g.n_tiles : cus;  // one workgroup per CU (LDS image)
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(block), kLdsBytes, s, a, g, ct);
@@ -957,15 +945,9 @@ int launch_blob_meta_chroma(const BlobArgs& a, const ChromaTables* ct, const Ran
   const int64_t total = (int64_t)a.n_frames * bh * cpr;
   if (total <= 0) return hipSuccess;
   if (total >= (1ll << 31)) return hipErrorInvalidValue;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(blob_chroma_meta_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBlobBytes);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  static int cus = 0;
-  if (!cus) cus = cu_count();
+  hipError_t e = set_dynamic_lds(reinterpret_cast<const void*>(blob_chroma_meta_kernel), (int)kLdsBlobBytes);
+  if (e != hipSuccess) return e;
+  const int cus = device_cus();
   BlobChromaGeom g;
   g.per_frame = make_div((uint32_t)(bh * cpr));
   g.per_row = make_div((uint32_t)cpr);

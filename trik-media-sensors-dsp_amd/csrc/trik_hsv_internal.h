@@ -114,7 +114,21 @@ struct KernelArgs {
   TrikHsvTargetSums* sums;
   uint8_t* masks;        // verification mode only
   int32_t mask_shift;    // bit position of this launch's range 0 in the mask byte
+  // Device-side kernel choice while the host does not know a new range set's
+  // exact-path share yet: with gate set the kernel runs only if
+  // (*gate <= gate_max) == gate_le (one uniform load per workgroup).
+  const unsigned long long* gate = nullptr;
+  unsigned long long gate_max = 0;
+  int32_t gate_le = 0;
 };
+
+__device__ __forceinline__ bool gated_out(const unsigned long long* gate, unsigned long long gate_max, int gate_le) {
+  return gate && ((*gate <= gate_max) != (gate_le != 0));
+}
+
+// The AUTO rule: the chroma-run kernel while a range group's expected
+// exact-path cost (ChromaTables::flagged_cost, share * 2^32) is at most this.
+constexpr unsigned long long kChromaMaxCost = (unsigned long long)(TRIK_HSV_CHROMA_MAX_SHARE * 4294967296.0);
 
 // RGB565X preview of N frames for one range (trik_hsv_operator.hip).
 struct PreviewArgs {
@@ -159,6 +173,12 @@ struct LineArgs {
   TrikHsvTarget* targets;            // may be NULL
 };
 
+// Per-device facts, cached thread-safely per device (trik_hsv_device.cpp):
+// the current device's CU count, and a kernel's dynamic-LDS attribute set once
+// per (device, kernel).
+int device_cus();
+hipError_t set_dynamic_lds(const void* kern, int bytes);
+
 // Launchers (trik_hsv_kernels.hip, trik_hsv_operator.hip, trik_hsv_line.hip).
 // Return hipError_t as int.
 int launch_reduce(const KernelArgs& a, bool write_masks, hipStream_t s);
@@ -200,6 +220,11 @@ struct BlobArgs {
   int32_t* n_labels;         // optional [n]
   int32_t meta_lds = 0;      // set by launch_blob: the bitmap staged in LDS
   int32_t meta_ready = 0;    // the bitmap is already written (launch_blob_meta_chroma)
+  // gate of the bitmap kernel (as KernelArgs::gate): the chroma-run bitmap and
+  // the stripe-arithmetic bitmap are both launched, one of them runs
+  const unsigned long long* gate = nullptr;
+  unsigned long long gate_max = 0;
+  int32_t gate_le = 0;
 };
 // Labels a frame can need: seeds are pairwise non-adjacent in the 8-neighbourhood
 // (a metapixel next to an earlier set one is never a seed), so at most

@@ -289,19 +289,7 @@ __global__ void synth_scene_kernel(uint8_t* frames, int64_t stride, int first_fr
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
-static int cu_count() {
-  static int cached[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 256;
-  if (dev < 0 || dev >= 64) return 256;
-  if (!cached[dev]) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-    cached[dev] = n;
-  }
-  return cached[dev];
-}
+static int cu_count() { return device_cus(); }
 
 template <int LAYOUT, int NR, bool MASKS, bool ALIGNED>
 static int launch_variant(const KernelArgs& a, hipStream_t s) {
@@ -314,12 +302,9 @@ static int launch_variant(const KernelArgs& a, hipStream_t s) {
   const int64_t grid = n_tiles < cap ? n_tiles : cap;
   const size_t lds = sizeof(RangeTables) + (kBlock / 64) * 3 * NR * sizeof(uint64_t);
   auto kern = reduce_kernel<LAYOUT, NR, MASKS, ALIGNED>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+  {
+    hipError_t e = set_dynamic_lds(reinterpret_cast<const void*>(kern), 80 * 1024);
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), lds, s, a, n_tiles, band,
                      tiles_per_frame);

@@ -379,20 +379,11 @@ static int launch_gather(const PreviewArgs& a, hipStream_t s) {
   const int64_t qpr = (a.out_ll + 3) / 4, total = (int64_t)a.n_frames * a.out_h * qpr;
   if (total >= (1ll << 31) || (!a.meta && !a.tables)) return hipErrorInvalidValue;
   if (total == 0) return hipSuccess;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(preview_gather_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+  {
+    hipError_t e = set_dynamic_lds(reinterpret_cast<const void*>(preview_gather_kernel), 80 * 1024);
     if (e != hipSuccess) return e;
-    attr = true;
   }
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-  }
+  const int cus = device_cus();
   PreviewGeom g;
   g.per_frame = make_div((uint32_t)(a.out_h * qpr));
   g.per_row = make_div((uint32_t)qpr);

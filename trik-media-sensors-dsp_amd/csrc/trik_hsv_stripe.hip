@@ -124,6 +124,7 @@ __device__ __forceinline__ uint32_t pack_bits(uint32_t e) {
 template <int LAYOUT, int NR, bool MASKS>
 __global__ __launch_bounds__(kMaxBlock) __attribute__((amdgpu_waves_per_eu(8)))
 void stripe_kernel(KernelArgs a, StripeGeom g) {
+  if (gated_out(a.gate, a.gate_max, a.gate_le)) return;
   {  // stage the tables at LDS address 0 (dynamic LDS, sizeof(StripeTables))
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     const u32x4* src = reinterpret_cast<const u32x4*>(a.stripe_tables);
@@ -276,20 +277,8 @@ void stripe_kernel(KernelArgs a, StripeGeom g) {
   }
 }
 
-int cu_count_stripe() {
-  int dev = 0, n = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 256;
-  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-    return 256;
-  return n;
-}
-
 // two workgroups per CU (LDS and VGPR budgets)
-int64_t stripe_slots() {
-  static int cus = 0;
-  if (!cus) cus = cu_count_stripe();
-  return 2LL * cus;
-}
+int64_t stripe_slots() { return 2LL * device_cus(); }
 
 // Tiles of <= kMaxSteps steps; small batches split each frame into more
 // (shorter) tiles until the grid fills the chip's workgroup slots -- one VGA
@@ -315,13 +304,9 @@ bool geometry(const KernelArgs& a, StripeGeom& g, int64_t slots) {
 template <int LAYOUT, int NR, bool MASKS>
 int launch_t(const KernelArgs& a, const StripeGeom& g, hipStream_t s) {
   auto kern = stripe_kernel<LAYOUT, NR, MASKS>;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)kLdsStripe);
+  {
+    hipError_t e = set_dynamic_lds(reinterpret_cast<const void*>(kern), (int)kLdsStripe);
     if (e != hipSuccess) return e;
-    attr = true;
   }
   const int block = ((g.k * g.cpr + 63) / 64) * 64;
   const int64_t slots = stripe_slots();

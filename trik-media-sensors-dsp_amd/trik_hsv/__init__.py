@@ -50,10 +50,11 @@ def frame_bytes(width: int, height: int, line_length: int, layout: int) -> int:
     return height * line_length * (2 if layout == LAYOUT_OV7670 else 1)
 
 
-def _stream_ptr(stream) -> C.c_void_p:
+def _stream_ptr(stream, tensor) -> C.c_void_p:
+    """`stream`, or torch's current stream of the device `tensor` lives on."""
     import torch
 
-    s = stream if stream is not None else torch.cuda.current_stream()
+    s = stream if stream is not None else torch.cuda.current_stream(tensor.device)
     return C.c_void_p(s.cuda_stream)
 
 
@@ -71,21 +72,47 @@ def _batch(frames, width, height, line_length, layout, n_frames=None, frame_stri
                            layout)
 
 
-class Detector:
+HOT_AUTO, HOT_STRIPE, HOT_CHROMA, HOT_GENERIC = 0, 1, 2, 3
+
+
+class _HotKernel:
+    """Hot-kernel selection of one handle (trik_hsv_set_hot_kernel)."""
+
+    def set_hot_kernel(self, kind: int) -> int:
+        """HOT_AUTO (the chroma-run kernel for large batches), HOT_STRIPE,
+        HOT_CHROMA or HOT_GENERIC for this handle's batched sums.  Returns the
+        previous setting.  Results are identical."""
+        prev = _lib.trik_hsv_set_hot_kernel(self._h, int(kind))
+        if prev < 0:
+            raise ValueError(f"unknown hot kernel {kind}")
+        return prev
+
+    def last_hot_kernel(self) -> int:
+        """The kernel this handle's last hot launch ran."""
+        return _lib.trik_hsv_last_hot_kernel(self._h)
+
+
+class Detector(_HotKernel):
     """Batched HSV-threshold + centroid over frames resident in device memory.
 
-    Owns one library handle (device tables are compiled per range set and
-    cached).  Methods enqueue on `stream` (default: torch's current stream)
-    and do not synchronise.
+    Owns one library handle, bound to `device` (default: the current device;
+    device tables are compiled per range set and cached).  Methods enqueue on
+    `stream` (default: torch's current stream of the frames' device) and do
+    not synchronise.
     """
 
-    def __init__(self):
+    def __init__(self, device=None, hot: int = HOT_AUTO):
+        import torch
+
         h = C.c_void_p()
         p = _default_params(0)
-        rc = _lib.TRIK_VIDTRANSCODE_CV_create(C.byref(p), C.byref(h))
+        with torch.cuda.device(device if device is not None else torch.cuda.current_device()):
+            rc = _lib.TRIK_VIDTRANSCODE_CV_create(C.byref(p), C.byref(h))
         if rc != IALG_EOK:
             raise TrikHsvError(rc, "TRIK_VIDTRANSCODE_CV_create")
         self._h = h
+        if hot != HOT_AUTO:
+            self.set_hot_kernel(hot)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -110,7 +137,7 @@ class Detector:
         if targets is None:
             targets = torch.empty((b.n_frames, T, 4), dtype=torch.int8, device=frames.device)
         rc = _lib.trik_hsv_process_batch(self._h, C.byref(b), arr, T, C.c_void_p(sums.data_ptr()),
-                                         C.c_void_p(targets.data_ptr()), _stream_ptr(stream))
+                                         C.c_void_p(targets.data_ptr()), _stream_ptr(stream, frames))
         if rc:
             raise TrikHsvError(rc, "trik_hsv_process_batch")
         return sums, targets
@@ -121,7 +148,7 @@ class Detector:
         b = _batch(frames, width, height, line_length, layout, n_frames, frame_stride)
         arr, T = _ranges(ranges)
         rc = _lib.trik_hsv_batch_sums(self._h, C.byref(b), arr, T, C.c_void_p(sums.data_ptr()),
-                                      _stream_ptr(stream))
+                                      _stream_ptr(stream, frames))
         if rc:
             raise TrikHsvError(rc, "trik_hsv_batch_sums")
         return sums
@@ -145,7 +172,7 @@ class Detector:
         masks = torch.zeros((b.n_frames, height, width), dtype=torch.uint8, device=frames.device)
         sums = torch.zeros((b.n_frames, T, 3), dtype=torch.int64, device=frames.device)
         rc = _lib.trik_hsv_batch_masks(self._h, C.byref(b), arr, T, C.c_void_p(masks.data_ptr()),
-                                       C.c_void_p(sums.data_ptr()), _stream_ptr(stream))
+                                       C.c_void_p(sums.data_ptr()), _stream_ptr(stream, frames))
         if rc:
             raise TrikHsvError(rc, "trik_hsv_batch_masks")
         return masks, sums
@@ -165,7 +192,7 @@ class Detector:
         arr, _ = _ranges([hsv_range])
         rc = _lib.trik_hsv_batch_preview(self._h, C.byref(b), arr, C.c_void_p(sums.data_ptr()),
                                          sums_pitch, ow, oh, oll, C.c_void_p(previews.data_ptr()),
-                                         oh * oll, _stream_ptr(stream))
+                                         oh * oll, _stream_ptr(stream, frames))
         if rc:
             raise TrikHsvError(rc, "trik_hsv_batch_preview")
         return previews
@@ -193,7 +220,7 @@ class Detector:
         alg = _abi.OV7670InArgsAlg(1, *[int(v) for v in hsv], 0)
         rc = _lib.trik_hsv_blob_batch(self._h, C.byref(b), C.byref(alg), ptr(out["targets"]), ptr(out["top"]),
                                       ptr(out["meta"]), ptr(out["labels"]), ptr(out["n_labels"]),
-                                      _stream_ptr(stream))
+                                      _stream_ptr(stream, frames))
         if rc:
             raise TrikHsvError(rc, "trik_hsv_blob_batch")
         return out
@@ -210,7 +237,7 @@ class Detector:
         previews = torch.empty((b.n_frames, oh, oll), dtype=torch.uint8, device=frames.device)
         rc = _lib.trik_hsv_blob_preview(self._h, C.byref(b), C.c_void_p(meta.data_ptr()),
                                         C.c_void_p(top.data_ptr()), ow, oh, oll,
-                                        C.c_void_p(previews.data_ptr()), oh * oll, _stream_ptr(stream))
+                                        C.c_void_p(previews.data_ptr()), oh * oll, _stream_ptr(stream, frames))
         if rc:
             raise TrikHsvError(rc, "trik_hsv_blob_preview")
         return previews
@@ -229,7 +256,7 @@ class Detector:
         previews = torch.empty((b.n_frames, oh, oll), dtype=torch.uint8, device=frames.device)
         rc = _lib.trik_hsv_line_preview(self._h, C.byref(b), int(val_from), int(val_to),
                                         C.c_void_p(sums.data_ptr()), ow, oh, oll,
-                                        C.c_void_p(previews.data_ptr()), oh * oll, _stream_ptr(stream))
+                                        C.c_void_p(previews.data_ptr()), oh * oll, _stream_ptr(stream, frames))
         if rc:
             raise TrikHsvError(rc, "trik_hsv_line_preview")
         return previews
@@ -249,7 +276,7 @@ def line_batch(frames, width, height, line_length, val_from, val_to, *, band=Non
     targets = torch.empty((b.n_frames, 4), dtype=torch.int8, device=frames.device)
     rc = _lib.trik_hsv_line_batch(C.byref(b), int(val_from), int(val_to), int(band[0]), int(band[1]),
                                   C.c_void_p(sums.data_ptr()), C.c_void_p(targets.data_ptr()),
-                                  _stream_ptr(stream))
+                                  _stream_ptr(stream, frames))
     if rc:
         raise TrikHsvError(rc, "trik_hsv_line_batch")
     return sums, targets
@@ -262,28 +289,10 @@ def batch_auto_range(frames, width, height, line_length, layout, *, n_frames=Non
 
     b = _batch(frames, width, height, line_length, layout, n_frames, frame_stride)
     out = torch.empty((b.n_frames, 6), dtype=torch.int16, device=frames.device)
-    rc = _lib.trik_hsv_batch_auto_range(C.byref(b), C.c_void_p(out.data_ptr()), _stream_ptr(stream))
+    rc = _lib.trik_hsv_batch_auto_range(C.byref(b), C.c_void_p(out.data_ptr()), _stream_ptr(stream, frames))
     if rc:
         raise TrikHsvError(rc, "trik_hsv_batch_auto_range")
     return out
-
-
-HOT_AUTO, HOT_STRIPE, HOT_CHROMA, HOT_GENERIC = 0, 1, 2, 3
-
-
-def set_hot_kernel(kind: int) -> int:
-    """Select the hot kernel of the batched sums (process-wide): HOT_AUTO (the
-    chroma-run kernel for large batches), HOT_STRIPE, HOT_CHROMA or
-    HOT_GENERIC.  Returns the previous setting.  Results are identical."""
-    prev = _lib.trik_hsv_set_hot_kernel(int(kind))
-    if prev < 0:
-        raise ValueError(f"unknown hot kernel {kind}")
-    return prev
-
-
-def last_hot_kernel() -> int:
-    """The kernel the last batched-sums launch on this thread ran."""
-    return _lib.trik_hsv_last_hot_kernel()
 
 
 def batch_targets(sums, width, height, *, stream=None):
@@ -294,7 +303,7 @@ def batch_targets(sums, width, height, *, stream=None):
     targets = torch.empty((N, T, 4), dtype=torch.int8, device=sums.device)
     b = _abi.FrameBatch(None, 0, N, width, height, 2 * width, LAYOUT_YUYV)
     rc = _lib.trik_hsv_batch_targets(C.byref(b), T, C.c_void_p(sums.data_ptr()),
-                                     C.c_void_p(targets.data_ptr()), _stream_ptr(stream))
+                                     C.c_void_p(targets.data_ptr()), _stream_ptr(stream, sums))
     if rc:
         raise TrikHsvError(rc, "trik_hsv_batch_targets")
     return targets
@@ -304,7 +313,7 @@ def synth(frames, width, height, line_length, layout, kind, seed, *, first_frame
           frame_stride=None, stream=None):
     """Fill a uint8 device tensor with synthetic frames (kind 0 uniform, 1 scene)."""
     b = _batch(frames, width, height, line_length, layout, n_frames, frame_stride)
-    rc = _lib.trik_hsv_synth(C.byref(b), first_frame, kind, seed, _stream_ptr(stream))
+    rc = _lib.trik_hsv_synth(C.byref(b), first_frame, kind, seed, _stream_ptr(stream, frames))
     if rc:
         raise TrikHsvError(rc, "trik_hsv_synth")
     return frames
@@ -346,7 +355,7 @@ def dynamic_params(width, height, line_length, out_width=320, out_height=240, ou
     return d
 
 
-class ObjectSensor:
+class ObjectSensor(_HotKernel):
     """One TRIK_VIDTRANSCODE_CV codec instance (vidtranscode_cv_fxns.c)."""
 
     _create = "TRIK_VIDTRANSCODE_CV_create"

@@ -10,8 +10,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# TRIK_HSV_LIB overrides the library path (development A/B of kernel variants)
-LIB_PATH = os.environ.get("TRIK_HSV_LIB") or os.path.join(HERE, "libtrik_hsv.so")
+LIB_PATH = os.path.join(HERE, "libtrik_hsv.so")
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
 
 # return codes / commands / bits (TI ialg.h, xdm.h values)
@@ -198,8 +197,8 @@ PROTOTYPES = {
     "trik_hsv_blob_preview": ([C.c_void_p, C.POINTER(FrameBatch), C.c_void_p, C.c_void_p, i32, i32, i32,
                                C.c_void_p, C.c_int64, C.c_void_p], i32),
     "trik_hsv_synth": ([C.POINTER(FrameBatch), i32, i32, u64, C.c_void_p], i32),
-    "trik_hsv_set_hot_kernel": ([i32], i32),
-    "trik_hsv_last_hot_kernel": ([], i32),
+    "trik_hsv_set_hot_kernel": ([C.c_void_p, i32], i32),
+    "trik_hsv_last_hot_kernel": ([C.c_void_p], i32),
     "trik_hsv_chroma_share": ([C.c_void_p, C.POINTER(C.c_double)], i32),
 }
 
@@ -223,10 +222,7 @@ def load() -> C.CDLL:
             raise ImportError(f"{LIB_PATH} is missing: build it with `make -C {CSRC}` "
                               "(or __graft_entry__.build()); there is no CPU fallback")
         L = C.CDLL(LIB_PATH)
-        dev_override = bool(os.environ.get("TRIK_HSV_LIB"))
         for name, (args, res) in PROTOTYPES.items():
-            if dev_override and not hasattr(L, name):
-                continue  # older library under A/B: only what it exports
             fn = getattr(L, name)
             fn.argtypes, fn.restype = args, res
         _lib = L
