@@ -35,15 +35,19 @@ SEED = 0x7A1C
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # 0.7 ms per step: 50 warmup steps bring the clocks to steady state (20
+    # steps after 3 warmups read ~10 % slow), 200 timed steps take 0.14 s
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--frames", type=int, default=4096, help="frames per GPU")
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--targets", type=int, default=4)
     ap.add_argument("--kind", type=int, default=0, help="0 uniform random bytes, 1 scene")
-    ap.add_argument("--cpu-frames", type=int, default=512, help="CPU baseline sample (frames)")
-    ap.add_argument("--cpu-frames-1core", type=int, default=32, help="single-thread CPU sample")
+    ap.add_argument("--cpu-frames", type=int, default=1024, help="CPU baseline sample (frames)")
+    ap.add_argument("--cpu-frames-1core", type=int, default=64, help="single-thread CPU sample")
+    ap.add_argument("--cpu-frames-emul", type=int, default=32,
+                    help="sample of the oracle's intrinsic-level emulation (secondary rate)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--hot", choices=["auto", "stripe", "chroma"], default="auto",
                     help="hot kernel (auto = the library's choice: chroma-run for this batch size)")
@@ -53,34 +57,47 @@ def parse():
 
 
 def cpu_baseline(args, width, height, ll, n_ranges, gpu_sums):
-    """Oracle (CPU port of the reference path) on a bounded sample; parity on it too."""
+    """CPU baseline on a bounded sample of the same frames: the clean-room scalar
+    restatement of the path (oracle/trik_cpu_baseline.c, a plain CPU port:
+    closed-form arithmetic, frames over POSIX threads), checked against the GPU
+    sums of those frames.  Threads: this process's CPU share (affinity and
+    OMP_NUM_THREADS; 16 per GPU on the bench box) -- the machine's total is
+    reported beside it, not used."""
     import numpy as np
 
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
 
+    machine = os.cpu_count() or 1
     try:
-        avail = len(os.sched_getaffinity(0))
+        allowed = len(os.sched_getaffinity(0))
     except AttributeError:
-        avail = os.cpu_count() or 1
-    cores = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail)), 64))
+        allowed = machine
+    omp = int(os.environ.get("OMP_NUM_THREADS", allowed))
+    cores = max(1, min(allowed, omp))
     n = min(args.cpu_frames, args.frames)
     host = oracle.synth(n, width, height, ll, oracle.LAYOUT_YUYV, args.kind, SEED)
+    rs = RANGES[:n_ranges]
     t0 = time.perf_counter()
-    sums, _ = oracle.batch(host, height * ll, n, width, height, ll, oracle.LAYOUT_YUYV,
-                           RANGES[:n_ranges], n_threads=cores)
+    sums = oracle.cpu_batch(host, height * ll, n, width, height, ll, oracle.LAYOUT_YUYV, rs, n_threads=cores)
     dt = time.perf_counter() - t0
     n1 = min(args.cpu_frames_1core, n)
     t1 = time.perf_counter()
-    oracle.batch(host, height * ll, n1, width, height, ll, oracle.LAYOUT_YUYV, RANGES[:n_ranges],
-                 n_threads=1)
+    oracle.cpu_batch(host, height * ll, n1, width, height, ll, oracle.LAYOUT_YUYV, rs, n_threads=1)
     dt1 = time.perf_counter() - t1
-    parity = bool(np.array_equal(sums, gpu_sums[:n]))
-    return {"value": round(n * width * height / dt / 1e6, 3), "unit": "Mpix/s", "cores": cores,
-            "kind": "port",
+    ne = min(args.cpu_frames_emul, n)
+    t2 = time.perf_counter()
+    emul, _ = oracle.batch(host, height * ll, ne, width, height, ll, oracle.LAYOUT_YUYV, rs, n_threads=cores)
+    dt2 = time.perf_counter() - t2
+    parity = bool(np.array_equal(sums, gpu_sums[:n])) and bool(np.array_equal(emul, gpu_sums[:ne]))
+    px = width * height
+    return {"value": round(n * px / dt / 1e6, 3), "unit": "Mpix/s", "cores": cores, "kind": "port",
+            "port": "clean-room scalar C restatement (oracle/trik_cpu_baseline.c), POSIX threads",
             "sample": f"{n} frames x {width}x{height} YUYV, {n_ranges} ranges "
                       f"(frames 0..{n - 1} of the GPU batch), {cores} threads, {dt:.2f} s",
-            "value_1core": round(n1 * width * height / dt1 / 1e6, 3),
+            "value_1core": round(n1 * px / dt1 / 1e6, 3),
+            "machine_threads": machine, "threads_allowed": allowed,
+            "value_intrinsic_emulation": round(ne * px / dt2 / 1e6, 3),
             "cpu_model": cpu_model()}, parity
 
 
@@ -152,6 +169,19 @@ def main():
         all_reduce_totals(batch_totals(sums))  # RCCL over xGMI when N > 1: 3*T int64 per step
         return targets
 
+    # cold batch: the first call with this range set compiles the range tables on
+    # the host, uploads them and builds the chroma-run tables on the device
+    # (stream-ordered, the host does not wait); timed apart from the steps
+    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    sums.zero_()
+    torch.cuda.synchronize()
+    c0.record(stream)
+    h0 = time.perf_counter()
+    det.batch_sums(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, ranges, sums, stream=stream)
+    host_call_ms = (time.perf_counter() - h0) * 1e3
+    c1.record(stream)
+    torch.cuda.synchronize()
+    cold_ms = c0.elapsed_time(c1)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -198,6 +228,11 @@ def main():
                      "kernel": f"{kname}<YUYV,{T}>", "kernel_ms": round(kern_ms, 4),
                      "kernel_ms_max_rank": round(kern_ms_max, 4),
                      "bytes_per_launch": bytes_per_launch},
+        # first call with a new range set (not in `value`): tables compiled,
+        # uploaded and built on the device, then the hot kernel; the host call
+        # returns before that work runs
+        "cold_batch": {"cold_batch_ms": round(cold_ms, 4), "table_build_ms": round(cold_ms - kern_ms, 4),
+                       "host_call_ms": round(host_call_ms, 4)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb, parity = cpu_baseline(args, W, H, ll, T, sums.cpu().numpy())

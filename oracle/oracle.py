@@ -99,6 +99,9 @@ def lib():
         L.trik_oracle_batch.argtypes = [vp, i64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                         vp, C.c_int, vp, vp, C.c_int]
         L.trik_oracle_batch.restype = C.c_int
+        L.trik_cpu_batch.argtypes = [vp, i64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                     vp, C.c_int, vp, C.c_int]
+        L.trik_cpu_batch.restype = C.c_int
         L.trik_oracle_synth.argtypes = [vp, i64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                         C.c_int, C.c_int, u64]
         L.trik_oracle_synth.restype = None
@@ -196,6 +199,18 @@ def batch(frames_u8: np.ndarray, frame_stride, n_frames, width, height, line_len
     if rc != 0:
         raise ValueError("oracle rejected batch")
     return sums, tg
+
+
+def cpu_batch(frames_u8: np.ndarray, frame_stride, n_frames, width, height, line_length, layout,
+              ranges, n_threads=1):
+    """The clean-room scalar CPU baseline (trik_cpu_baseline.c): sums[N,T,3] int64."""
+    rs = list(ranges)
+    sums = np.zeros((n_frames, len(rs), 3), np.int64)
+    rc = lib().trik_cpu_batch(_ptr(frames_u8), frame_stride, n_frames, width, height, line_length,
+                              layout, ranges_array(rs), len(rs), _ptr(sums), n_threads)
+    if rc != 0:
+        raise ValueError("cpu baseline rejected batch")
+    return sums
 
 
 def synth(n_frames, width, height, line_length, layout, kind, seed, first_frame=0,

@@ -113,6 +113,15 @@ int      trik_oracle_batch(const uint8_t* frames, int64_t frame_stride, int n_fr
                            const trik_oracle_range* ranges, int n_ranges,
                            int64_t* sums, int8_t* targets, int n_threads);
 
+/* The clean-room scalar CPU baseline (trik_cpu_baseline.c): the same sums as
+ * trik_oracle_batch (n_ranges <= 32), computed the way a plain CPU port would
+ * (closed-form arithmetic, no intrinsic emulation), frames split over
+ * n_threads POSIX threads.  Used by bench.py's cpu_baseline only. */
+int      trik_cpu_batch(const uint8_t* frames, int64_t frame_stride, int n_frames,
+                        int width, int height, int line_length, int layout,
+                        const trik_oracle_range* ranges, int n_ranges, int64_t* sums,
+                        int n_threads);
+
 /* Synthetic frame generators shared bit-for-bit with the device generator
  * (synth kernels in trik-media-sensors-dsp_amd/csrc/trik_hsv_kernels.hip).
  * kind 0 = uniform random bytes, kind 1 = scene (gradients + 6 discs). */

@@ -31,7 +31,7 @@ def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     oracle.build()
     P = tcm.profiles(oracle, tcm.BENCH[:n])
-    runs, blocks = tcm.build(P)
+    runs, blocks, _cut = tcm.build(P)
     Y = np.arange(256)[None, :]
     b1, b2 = (runs & 255)[:, None], (runs >> 8)[:, None]
     x = (runs == tcm.KEXC)

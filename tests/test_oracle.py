@@ -162,3 +162,20 @@ def test_epilogue_edges(oracle_mod):
     x, y, s = oracle_mod.targets([n, sx, sy], 640, 480)
     assert (x, y) == (0, 0)  # cx=319 -> (319-320)*200/640 truncates to 0
     assert s == (313 * 400) // 1120
+
+
+# --- the clean-room scalar CPU baseline (bench.py cpu_baseline) equals the oracle ---
+@pytest.mark.parametrize("layout,kind,n_ranges", [(0, 0, 4), (0, 1, 4), (1, 1, 2), (0, 1, 12), (1, 0, 1)])
+def test_cpu_baseline_equals_oracle(oracle_mod, layout, kind, n_ranges):
+    o = oracle_mod
+    ranges = [(0, 30, 50, 100, 30, 100), (90, 150, 40, 100, 20, 100), (200, 260, 40, 100, 20, 100),
+              (330, 20, 30, 100, 30, 100), (0, 359, 0, 100, 0, 100), (10, 10, 0, 100, 0, 100),
+              (359, 0, 0, 100, 0, 100), (45, 300, 5, 95, 5, 95), (120, 121, 50, 51, 50, 51),
+              (0, 359, 0, 0, 0, 0), (180, 179, 0, 100, 0, 100), (-5, 400, -1, 200, -1, 200)][:n_ranges]
+    w, h = 320, 240
+    ll = 2 * w if layout == o.LAYOUT_YUYV else w + 32
+    stride = h * ll * (2 if layout == o.LAYOUT_OV7670 else 1)
+    frames = o.synth(6, w, h, ll, layout, kind, 0x51 + kind)
+    want, _ = o.batch(frames, stride, 6, w, h, ll, layout, ranges)
+    got = o.cpu_batch(frames, stride, 6, w, h, ll, layout, ranges, n_threads=3)
+    assert np.array_equal(got, want)

@@ -48,6 +48,12 @@ constexpr int kMaxBlock = 1024;
 #ifndef TRIK_CHROMA_NT
 #define TRIK_CHROMA_NT 1  // YUYV frame loads with the nontemporal hint
 #endif
+#ifndef TRIK_CHROMA_SPLITB
+#define TRIK_CHROMA_SPLITB 0  // block words as two byte tables (pair offset, cut): -3 VALU per word, but one more LDS read; measured slower
+#endif
+#ifndef TRIK_CHROMA_Q2
+#define TRIK_CHROMA_Q2 1  // queue appends batched per step, EXEC-masked stores without branches
+#endif
 #ifndef TRIK_CHROMA_CW
 #define TRIK_CHROMA_CW 8
 #endif
@@ -58,9 +64,9 @@ constexpr int kMaxSteps = kChunkWords == 8 ? 31 : 63;
 static_assert((kChunkWords == 8 ? 4 : 2) * 2 * kMaxSteps <= 255, "flush group sums fit a byte");
 constexpr int kQFlush = 7;
 constexpr int kQueueCap = 128;  // blob kernel, entries per wave: < 64 waiting + <= 64 added by one word slot
-// Hot kernel: at most 15 waves (960 lanes) per workgroup; a wave drains when
-// its queue holds >= kDrainAt entries, checked after every second word slot,
-// so the queue holds < kDrainAt + 128 entries.
+// Hot kernel: at most 15 waves (960 lanes) per workgroup; a wave drains its
+// queue down to < kDrainAt entries after every step, and a step appends its
+// words at once when they fit (else word by word, draining before each).
 constexpr int kHotLanes = 960;
 constexpr int kDrainAt = 60;
 constexpr int kHotQueueCap = kDrainAt - 1 + 128;
@@ -78,6 +84,11 @@ constexpr uint32_t kLdsVal = kLdsSat + 256;           // u8  [256]   value test 
 constexpr uint32_t kLdsRuns = kLdsVal + 256;          // u16 [65536] b1 | b2 << 8 per chroma
 constexpr uint32_t kLdsQueues = kLdsRuns + 131072;    // per wave: kHotQueueCap (blob: kQueueCap) x {word, pos}
 static_assert(kLdsBlocks + 8192 <= kLdsPairs, "LDS layout");
+// The hot kernel keeps the block words as two byte tables in the same 8 KiB:
+// the pair's palette offset and the cut, both indexed by the block c >> 4
+// (one shift for both addresses; the offset byte is the pair's address).
+constexpr uint32_t kLdsBlkPair = kLdsBlocks;          // u8 [4096]
+constexpr uint32_t kLdsBlkCut = kLdsBlocks + 4096;    // u8 [4096]
 constexpr uint32_t kLdsBytes = kLdsQueues + (kHotLanes / 64) * kHotQueueCap * 8;
 static_assert(kLdsBytes <= 160 * 1024, "chroma kernel LDS image");
 
@@ -107,20 +118,30 @@ __device__ __forceinline__ void st64(uint32_t a, uint32_t x, uint32_t y) {
 // le, where the select gives 0; windows lie above the cut) or any pixel of an
 // exception-code word (le is cleared, so the select gives 0 as well).  vm
 // masks lanes without a valid row.
+#define TRIK_SELECT2_CMPS(AB)                                                                   \
+  "v_cmp_eq_u32_e64 %[x], %[k], %[d]\n\t"                                                       \
+  "v_cmp_gt_u32_sdwa %[lt0], %[d], %[w] src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"                    \
+  "v_cmp_gt_u32_sdwa %[lt1], %[d], %[w] src0_sel:BYTE_0 src1_sel:BYTE_2\n\t"                    \
+  "v_cmp_ge_u32_sdwa %[le0], %[d], %[w] src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"                    \
+  "v_cmp_ge_u32_sdwa %[le1], %[d], %[w] src0_sel:BYTE_1 src1_sel:BYTE_2\n\t"                    \
+  "v_cmp_le_u32_sdwa %[ge0], %[a], %[w] src0_sel:BYTE_" #AB " src1_sel:BYTE_0\n\t"              \
+  "v_cmp_le_u32_sdwa %[ge1], %[a], %[w] src0_sel:BYTE_" #AB " src1_sel:BYTE_2"
+// ABYTE: the byte of bw holding the cut A
+template <int ABYTE = 1>
 __device__ __forceinline__ void select2(uint32_t w, uint32_t d, uint32_t bw, uint32_t m1, uint32_t m2, uint64_t vm,
                                         uint32_t& e0, uint32_t& e1, uint64_t& q0, uint64_t& q1) {
+  static_assert(ABYTE == 0 || ABYTE == 1, "cut byte");
   uint64_t x, lt0, lt1, le0, le1, ge0, ge1;
-  asm volatile(
-      "v_cmp_eq_u32_e64 %[x], %[k], %[d]\n\t"
-      "v_cmp_gt_u32_sdwa %[lt0], %[d], %[w] src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"
-      "v_cmp_gt_u32_sdwa %[lt1], %[d], %[w] src0_sel:BYTE_0 src1_sel:BYTE_2\n\t"
-      "v_cmp_ge_u32_sdwa %[le0], %[d], %[w] src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"
-      "v_cmp_ge_u32_sdwa %[le1], %[d], %[w] src0_sel:BYTE_1 src1_sel:BYTE_2\n\t"
-      "v_cmp_le_u32_sdwa %[ge0], %[a], %[w] src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"
-      "v_cmp_le_u32_sdwa %[ge1], %[a], %[w] src0_sel:BYTE_1 src1_sel:BYTE_2"
-      : [x] "=&s"(x), [lt0] "=&s"(lt0), [lt1] "=&s"(lt1), [le0] "=&s"(le0), [le1] "=&s"(le1), [ge0] "=&s"(ge0),
-        [ge1] "=&s"(ge1)
-      : [w] "v"(w), [d] "v"(d), [a] "v"(bw), [k] "s"(kChromaExc));
+  if constexpr (ABYTE == 1)
+    asm volatile(TRIK_SELECT2_CMPS(1)
+                 : [x] "=&s"(x), [lt0] "=&s"(lt0), [lt1] "=&s"(lt1), [le0] "=&s"(le0), [le1] "=&s"(le1),
+                   [ge0] "=&s"(ge0), [ge1] "=&s"(ge1)
+                 : [w] "v"(w), [d] "v"(d), [a] "v"(bw), [k] "s"(kChromaExc));
+  else
+    asm volatile(TRIK_SELECT2_CMPS(0)
+                 : [x] "=&s"(x), [lt0] "=&s"(lt0), [lt1] "=&s"(lt1), [le0] "=&s"(le0), [le1] "=&s"(le1),
+                   [ge0] "=&s"(ge0), [ge1] "=&s"(ge1)
+                 : [w] "v"(w), [d] "v"(d), [a] "v"(bw), [k] "s"(kChromaExc));
   q0 = (x | (lt0 & ~le0)) & vm;
   q1 = (x | (lt1 & ~le1)) & vm;
   const uint64_t k0 = le0 & ge0 & ~x & vm, k1 = le1 & ge1 & ~x & vm;
@@ -131,6 +152,21 @@ __device__ __forceinline__ void select2(uint32_t w, uint32_t d, uint32_t bw, uin
       "v_cndmask_b32_e64 %[e1], 0, %[e1], %[k1]"
       : [e0] "=&v"(e0), [e1] "=&v"(e1)
       : [m1] "v"(m1), [m2] "v"(m2), [lt0] "s"(lt0), [lt1] "s"(lt1), [k0] "s"(k0), [k1] "s"(k1));
+}
+
+// Queue store of (w, pos) at LDS address qa by the lanes of wave mask m only:
+// EXEC narrowed and restored inside one asm block (no branch, so the stores
+// of a step's words stay in one basic block).  The compiler's own LDS
+// counters stay conservative: LDS operations of a wave complete in order.
+__device__ __forceinline__ void store_masked(uint64_t m, uint32_t qa, uint32_t w, uint32_t pos) {
+  uint64_t saved;
+  asm volatile(
+      "s_and_saveexec_b64 %[sv], %[m]\n\t"
+      "ds_write2_b32 %[a], %[w], %[p] offset1:1\n\t"
+      "s_mov_b64 exec, %[sv]"
+      : [sv] "=&s"(saved)
+      : [m] "s"(m), [a] "v"(qa), [w] "v"(w), [p] "v"(pos)
+      : "memory", "scc");
 }
 
 // 4-bit mask (range t -> bit t) -> byte-spread (range t -> bit 8t)
@@ -325,24 +361,34 @@ __global__ __launch_bounds__(256) void chroma_palette_kernel(ChromaTables* ct) {
 // rstep = k); ov7670: one 16-pixel piece (dy = dx = 0, rstep = k).
 struct ChromaGeom {
   int32_t cpr, k, rstep, dy, dx, steps, tiles_per_frame;
+  int32_t steps_last;  // steps of a frame's last tile
   int64_t n_tiles;
   int32_t flush_rounds;  // drain rounds between unpacks of the 16-bit exception sums
 };
 
-template <int N>
-__device__ __forceinline__ void wave_sums(uint32_t (&v)[N]) {
+// The 12 per-lane values (3 per range, 4 ranges) summed over the wave: two
+// lane-half swaps (permlane32 / permlane16) leave three values per lane, each
+// the partial sum of one value over lanes 16 apart, then four DPP row steps.
+// Value i + 3 * r ends in lane 16 r + 15 (r = 0..3) of v[i], i = 0..2.
+__device__ __forceinline__ void wave_sums12(uint32_t (&v)[12]) {
 #pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x111, 0xF, 0xF, true);
+  for (int i = 0; i < 6; ++i) {
+    const auto s = __builtin_amdgcn_permlane32_swap(v[i], v[i + 6], false, false);
+    v[i] = s[0] + s[1];
+  }
 #pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x112, 0xF, 0xF, true);
+  for (int i = 0; i < 3; ++i) {
+    const auto s = __builtin_amdgcn_permlane16_swap(v[i], v[i + 3], false, false);
+    v[i] = s[0] + s[1];
+  }
 #pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x114, 0xF, 0xF, true);
+  for (int i = 0; i < 3; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x111, 0xF, 0xF, true);
 #pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x118, 0xF, 0xF, true);
+  for (int i = 0; i < 3; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x112, 0xF, 0xF, true);
 #pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x142, 0xA, 0xF, false);
+  for (int i = 0; i < 3; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x114, 0xF, 0xF, true);
 #pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x143, 0xC, 0xF, false);
+  for (int i = 0; i < 3; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x118, 0xF, 0xF, true);
 }
 
 // One chunk = CW YUYV words (2*CW pixels): YUYV, two 16-byte pieces (8
@@ -423,9 +469,17 @@ template <int LAYOUT, int NR, bool MASKS, int CW>
 __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaGeom g, const ChromaTables* ct) {
   if (gated_out(a.gate, a.gate_max, a.gate_le)) return;
   const int t = threadIdx.x;
-  {  // stage block masks, the mask-pair table and the run descriptors
+  {  // stage the block bytes, the mask-pair table and the run descriptors
+#if TRIK_CHROMA_SPLITB
+    for (int i = t; i < 4096 / 4; i += blockDim.x) {  // 4 block words -> 4 pair bytes + 4 cut bytes
+      const u32x2 bw = reinterpret_cast<const u32x2*>(ct->blocks)[i];
+      *(lds32_t)(uintptr_t)(kLdsBlkPair + 4 * i) = __builtin_amdgcn_perm(bw.y, bw.x, 0x06040200u);
+      *(lds32_t)(uintptr_t)(kLdsBlkCut + 4 * i) = __builtin_amdgcn_perm(bw.y, bw.x, 0x07050301u);
+    }
+#else
     for (int i = t; i < 8192 / 16; i += blockDim.x)
       *(lds128_t)(uintptr_t)(kLdsBlocks + 16 * i) = reinterpret_cast<const u32x4*>(ct->blocks)[i];
+#endif
     for (int i = t; i < kChromaPalette; i += blockDim.x) st64(kLdsPairs + 8 * i, ct->palette[2 * i], ct->palette[2 * i + 1]);
     for (int i = t; i < 131072 / 16; i += blockDim.x)
       *(lds128_t)(uintptr_t)(kLdsRuns + 16 * i) = reinterpret_cast<const u32x4*>(ct->runs)[i];
@@ -460,12 +514,18 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
 
   const int64_t t_begin = g.n_tiles * blockIdx.x / gridDim.x;
   const int64_t t_end = g.n_tiles * (blockIdx.x + 1) / gridDim.x;
+  // the frame and the tile within it, stepped along (wave-uniform, SALU)
+  int fcur = __builtin_amdgcn_readfirstlane((int)(t_begin / g.tiles_per_frame));
+  int trem = __builtin_amdgcn_readfirstlane((int)(t_begin - (int64_t)fcur * g.tiles_per_frame));
   for (int64_t tile = t_begin; tile < t_end; ++tile) {
-    const int f = (int)(tile / g.tiles_per_frame);
-    const int r0 = (int)(tile - (int64_t)f * g.tiles_per_frame) * g.rstep * g.steps;
+    const int r0 = trem * g.rstep * g.steps;
     const int y0 = r0 + ro;
-    // wave-uniform (the division runs on the VALU): keeps the step loop scalar
-    const int steps = __builtin_amdgcn_readfirstlane(min(g.steps, (a.height - r0 + g.rstep - 1) / g.rstep));
+    const int steps = trem == g.tiles_per_frame - 1 ? g.steps_last : g.steps;
+    const int f = fcur;
+    if (++trem == g.tiles_per_frame) {
+      trem = 0;
+      ++fcur;
+    }
     const uint8_t* p = a.frames + (int64_t)f * a.frame_stride + (int64_t)y0 * a.line_length + col_bytes;
 
     uint32_t P[CW], O = 0, Q = 0, CumS = 0, CumA = 0, CumB = 0;
@@ -527,9 +587,13 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     // a row inside the frame for lanes whose rows run past it (re-read, masked)
     const uint8_t* pf = active && y0 < a.height ? p : a.frames + (int64_t)f * a.frame_stride + col_bytes;
     // steps whose first (second) piece row lies inside the frame
-    const int vsteps = active ? max(0, min(steps, (a.height - y0 + g.rstep - 1) / g.rstep)) : 0;
-    const int vstepsb = active ? max(0, min(steps, (a.height - y0 - half + g.rstep - 1) / g.rstep)) : 0;
     const bool full = (r0 + steps * g.rstep <= a.height) && (g.k * g.cpr) % 64 == 0;
+    // (only partial tiles need them: the divisions run on the VALU)
+    int vsteps = steps, vstepsb = steps;
+    if (!full) {
+      vsteps = active ? max(0, min(steps, (a.height - y0 + g.rstep - 1) / g.rstep)) : 0;
+      vstepsb = active ? max(0, min(steps, (a.height - y0 - half + g.rstep - 1) / g.rstep)) : 0;
+    }
     const uint8_t* tbase = a.frames + (int64_t)f * a.frame_stride + (int64_t)r0 * a.line_length;
     auto run = [&](auto full_c) {
       constexpr bool FULL = decltype(full_c)::value;
@@ -542,7 +606,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         // their pixels are masked out of the sums and the queue)
         const uint64_t vma = FULL ? ~0ull : __builtin_amdgcn_ballot_w64(valid);
         const uint64_t vmb = FULL ? ~0ull : (SPLIT ? __builtin_amdgcn_ballot_w64(validb) : vma);
-        uint32_t c[CW], d[CW], cut[CW], e[2 * CW];
+        uint32_t c[CW], d[CW], cut[CW], pr[CW], e[2 * CW];
         u32x2 mm[CW];
 #pragma unroll
         for (int i = 0; i < CW; ++i) c[i] = chroma_of(cw[i]);
@@ -553,8 +617,16 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
           cut[i] = 8u * (c[i] >> 12);
 #else
           d[i] = ld16(kLdsRuns + 2u * c[i]);
+#if TRIK_CHROMA_SPLITB
+          // the block c >> 4: its pair's palette offset and its cut, two bytes
+          const uint32_t b = c[i] >> 4;
+          pr[i] = ld8(kLdsBlkPair + b);
+          cut[i] = ld8(kLdsBlkCut + b);
+#else
           // the block word: the pair's palette offset | the cut << 8
           cut[i] = ld16(kLdsBlocks + ((c[i] >> 3) & 0x1FFEu));
+          pr[i] = cut[i] & 0xFFu;
+#endif
 #endif
         }
 #ifdef TRIK_AB_NO_LDS
@@ -562,7 +634,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         for (int i = 0; i < CW; ++i) { mm[i].x = cut[i] & 0x01010101u; mm[i].y = (cut[i] >> 1) & 0x01010101u; }
 #else
 #pragma unroll
-        for (int i = 0; i < CW; ++i) mm[i] = ld64(kLdsPairs + (cut[i] & 0xFFu));
+        for (int i = 0; i < CW; ++i) mm[i] = ld64(kLdsPairs + pr[i]);
 #endif
         // pin the descriptors as 32-bit values here (ds_read_u16 zero-extends):
         // otherwise the zero extension is sunk past the drain branches and
@@ -573,6 +645,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         // path (a wave mask in SGPRs) are queued
         const uint32_t pos_s = x0 | ((uint32_t)(ro + s * g.rstep) << 16);
         const uint32_t pos_b = pos_s + ((uint32_t)half << 16);
+        uint64_t bal[CW];
 #pragma unroll
         for (int i = 0; i < CW; ++i) {
           uint64_t q0, q1;
@@ -581,9 +654,10 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
           e[2 * i + 1] = (cw[i] >> 1) & 0x01010101u;
           q0 = q1 = 0;
 #else
-          select2(cw[i], d[i], cut[i], mm[i].x, mm[i].y, i < 4 ? vma : vmb, e[2 * i], e[2 * i + 1], q0, q1);
+          select2<TRIK_CHROMA_SPLITB ? 0 : 1>(cw[i], d[i], cut[i], mm[i].x, mm[i].y, i < 4 ? vma : vmb, e[2 * i],
+                                              e[2 * i + 1], q0, q1);
 #endif
-          const uint64_t bal = q0 | q1;
+          bal[i] = q0 | q1;
           if (MASKS && (i < 4 ? valid : validb)) {  // verification mode: the exact path writes the flagged pixels
             const int y = y0 + s * g.rstep + (i < 4 ? 0 : half);
             uint8_t* mp = a.masks + ((int64_t)f * a.height + y) * a.width + x0 + xoff(i);
@@ -592,25 +666,69 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
             if (!__builtin_amdgcn_inverse_ballot_w64(q0)) mp[0] = a.mask_shift ? (uint8_t)(mp[0] | m0) : m0;
             if (!__builtin_amdgcn_inverse_ballot_w64(q1)) mp[1] = a.mask_shift ? (uint8_t)(mp[1] | m1) : m1;
           }
+        }
 #ifndef TRIK_AB_NO_ENQUEUE  // timing attribution only (drops the exception words)
-          // (a branch on bal != 0 would seldom skip: some lane of the wave has a
-          // flagged word in most slots)
-          const uint32_t idx =
-              __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-          if (__builtin_amdgcn_inverse_ballot_w64(bal)) {
-            const uint32_t qa = __builtin_amdgcn_readfirstlane(qbase_s + 8u * (uint32_t)qn) + 8u * idx;
+        // The words with a pixel for the exact path are appended to the
+        // wave's queue at their rank among the slot's flagged lanes.  (A branch
+        // on a slot's mask would seldom skip: some lane of the wave has a
+        // flagged word in most slots.)
+        auto rank = [](uint64_t m) {
+          return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        };
+#if TRIK_CHROMA_Q2
+        int total = 0;
+#pragma unroll
+        for (int i = 0; i < CW; ++i) total += __builtin_popcountll(bal[i]);
+        // the whole step fits nearly always (qn < kDrainAt here, total ~15 of
+        // at most 512): one basic block of EXEC-masked stores, no branch and
+        // no drain check between the words; otherwise the queue is emptied
+        // first, and a step with more flagged words than the queue holds
+        // (never seen) stores word by word, emptying it after each
+        if (qn + total > kHotQueueCap)
+          while (qn > 0) drain(qn < 64 ? qn : 64);
+        if (total <= kHotQueueCap) {
+          // entry index = the entries before this slot + the lane's rank (mbcnt
+          // accumulates the scalar count)
+          uint32_t at = (uint32_t)qn;
+#pragma unroll
+          for (int i = 0; i < CW; ++i) {
+            const uint32_t idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[i] >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bal[i], at));
+            store_masked(bal[i], qbase_s + 8u * idx, cw[i], (i < 4 ? pos_s : pos_b) + xoff(i));
+            at += (uint32_t)__builtin_popcountll(bal[i]);
+          }
+          qn += total;
+        } else {
+          for (int i = 0; i < CW; ++i) {
+            const uint32_t qoff = __builtin_amdgcn_readfirstlane(qbase_s + 8u * (uint32_t)qn);
+            store_masked(bal[i], qoff + 8u * rank(bal[i]), cw[i], (i < 4 ? pos_s : pos_b) + xoff(i));
+            qn += __builtin_popcountll(bal[i]);
+            while (qn > 0) drain(qn < 64 ? qn : 64);
+          }
+        }
+#ifdef TRIK_AB_NO_DRAIN  // timing attribution only (drops the exception words)
+        if (qn >= kDrainAt) qn = 0;
+#else
+        while (qn >= kDrainAt) drain(qn < 64 ? qn : 64);
+#endif
+#else
+#pragma unroll
+        for (int i = 0; i < CW; ++i) {
+          if (__builtin_amdgcn_inverse_ballot_w64(bal[i])) {
+            const uint32_t qa = __builtin_amdgcn_readfirstlane(qbase_s + 8u * (uint32_t)qn) + 8u * rank(bal[i]);
             *(lds32_t)(uintptr_t)qa = cw[i];
             *(lds32_t)(uintptr_t)(qa + 4u) = (i < 4 ? pos_s : pos_b) + xoff(i);
           }
-          qn += __builtin_popcountll(bal);
-#ifdef TRIK_AB_NO_DRAIN  // timing attribution only (drops the exception words)
+          qn += __builtin_popcountll(bal[i]);
+#ifdef TRIK_AB_NO_DRAIN
           if ((i & 1) && qn >= kDrainAt) qn = 0;
 #else
           if (i & 1)
             while (qn >= kDrainAt) drain(qn < 64 ? qn : 64);
 #endif
-#endif
         }
+#endif
+#endif
 #pragma unroll
         for (int i = 0; i < CW; ++i) P[i] = P[i] + e[2 * i] + e[2 * i + 1];
 #pragma unroll
@@ -681,27 +799,36 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     for (int rr = 0; rr < NR; ++rr) {
       const int sh = 8 * rr;
       const uint32_t c = ((rr & 1) ? (CumB >> ((rr >> 1) * 16)) : (CumA >> ((rr >> 1) * 16))) & 0xFFFFu;
-      uint32_t wx = (O >> sh) & 0xFFu, nb2 = 0;  // nb2: pixels of the second pieces (rows + half)
+      // x offsets within the chunk: 2 (i & 3) (+ dx for the second piece) or 2 i;
+      // nb2: pixels of the second pieces (rows + half, columns + dx)
+      uint32_t wx = (O >> sh) & 0xFFu, nb2 = 0;
 #pragma unroll
-      for (int i = 1; i < CW; ++i) wx += xoff(i) * ((P[i] >> sh) & 0xFFu);
+      for (int i = 1; i < CW; ++i) wx += (uint32_t)(SPLIT ? 2 * (i & 3) : 2 * i) * ((P[i] >> sh) & 0xFFu);
       if (SPLIT) {
 #pragma unroll
         for (int i = 4; i < CW; ++i) nb2 += (P[i] >> sh) & 0xFFu;
+        wx += __umul24(dx, nb2);
       }
       const uint32_t qq = ((rr & 1) ? (Qb >> ((rr >> 1) * 16)) : (Qa >> ((rr >> 1) * 16))) & 0xFFFFu;
       acc[3 * rr + 0] = c + xacc[3 * rr + 0];
-      acc[3 * rr + 1] = x0 * c + wx + xacc[3 * rr + 1];
-      acc[3 * rr + 2] = (uint32_t)y0 * c + (uint32_t)g.rstep * ((uint32_t)steps * c - qq) +
-                        (uint32_t)half * nb2 + xacc[3 * rr + 2];
+      acc[3 * rr + 1] = __umul24(x0, c) + wx + xacc[3 * rr + 1];
+      acc[3 * rr + 2] = __umul24((uint32_t)y0, c) + (uint32_t)g.rstep * ((uint32_t)steps * c - qq) +
+                        __umul24((uint32_t)half, nb2) + xacc[3 * rr + 2];
     }
-    wave_sums<3 * NR>(acc);
-    if (lane == 63) {
-      TrikHsvTargetSums* dst = a.sums + (int64_t)f * a.sums_ranges + a.range_offset;
+    uint32_t red[12];
 #pragma unroll
-      for (int v = 0; v < 3 * NR; ++v)
-        if (acc[v])
-          atomicAdd(reinterpret_cast<unsigned long long*>(&dst[v / 3].points) + (v % 3),
-                    (unsigned long long)acc[v]);
+    for (int v = 0; v < 12; ++v) red[v] = v < 3 * NR ? acc[v] : 0u;
+    wave_sums12(red);
+    if ((lane & 15) == 15) {
+      // lane 16 r + 15 holds values 3 r .. 3 r + 2: range r's N, sum x, sum y
+      const int rr = lane >> 4;
+      if (rr < NR) {
+        unsigned long long* dst =
+            reinterpret_cast<unsigned long long*>(&a.sums[(int64_t)f * a.sums_ranges + a.range_offset + rr].points);
+#pragma unroll
+        for (int v = 0; v < 3; ++v)
+          if (red[v]) atomicAdd(dst + v, (unsigned long long)red[v]);
+      }
     }
   }
 }
@@ -906,6 +1033,8 @@ bool chroma_geometry(const KernelArgs& a, ChromaGeom& g) {
   const int steps_total = (a.height + g.rstep - 1) / g.rstep;
   g.tiles_per_frame = (steps_total + kMaxSteps - 1) / kMaxSteps;
   g.steps = (steps_total + g.tiles_per_frame - 1) / g.tiles_per_frame;
+  g.tiles_per_frame = (steps_total + g.steps - 1) / g.steps;  // every tile has >= 1 step
+  g.steps_last = steps_total - (g.tiles_per_frame - 1) * g.steps;
   g.n_tiles = (int64_t)g.tiles_per_frame * a.n_frames;
   // per drain round a lane adds <= 2 pixels: byte counts <= 2r, x sums <= 2r*W,
   // row sums <= 2r*rows; the 16-bit sums must take at least one round
