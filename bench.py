@@ -32,6 +32,19 @@ RANGES = [(0, 30, 50, 100, 30, 100), (90, 150, 40, 100, 20, 100),
 SEED = 0x7A1C
 
 
+# BASELINE.json configs: C3 (the metric's config) and C4 (1280x720, 2 targets)
+WORKLOADS = {"c3": dict(frames=4096, width=640, height=480, targets=4),
+             "c4": dict(frames=1024, width=1280, height=720, targets=2)}
+
+
+def workload_name(wl, per_gpu, total, world, w, h, t):
+    name = f"{wl.upper()}: batch {per_gpu} x {w}x{h} YUYV per GPU, {t} HSV targets"
+    if world > 1:
+        c5 = total == 32768 and (w, h, t) == (640, 480, 4)
+        name += f"; {total} frames over {world} GPUs" + (" (C5)" if c5 else "")
+    return name
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -39,10 +52,14 @@ def parse():
     # steps after 3 warmups read ~10 % slow), 200 timed steps take 0.14 s
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--frames", type=int, default=4096, help="frames per GPU")
-    ap.add_argument("--width", type=int, default=640)
-    ap.add_argument("--height", type=int, default=480)
-    ap.add_argument("--targets", type=int, default=4)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3",
+                    help="c3 (the headline: 4096 x 640x480, 4 targets) or c4 (1024 x 1280x720, 2 targets)")
+    ap.add_argument("--frames", type=int, default=None, help="frames per GPU (default: the workload's)")
+    ap.add_argument("--total-frames", type=int, default=None,
+                    help="strong scaling: this many frames split over the ranks (C5: 32768)")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--targets", type=int, default=None)
     ap.add_argument("--kind", type=int, default=0, help="0 uniform random bytes, 1 scene")
     ap.add_argument("--cpu-frames", type=int, default=1024, help="CPU baseline sample (frames)")
     ap.add_argument("--cpu-frames-1core", type=int, default=64, help="single-thread CPU sample")
@@ -53,7 +70,11 @@ def parse():
                     help="hot kernel (auto = the library's choice: chroma-run for this batch size)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="rocprofv3 FETCH_SIZE summary used for roofline.traffic")
-    return ap.parse_args()
+    args = ap.parse_args()
+    for k, v in WORKLOADS[args.workload].items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
+    return args
 
 
 def cpu_baseline(args, width, height, ll, n_ranges, gpu_sums):
@@ -145,14 +166,20 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    W, H, F, T = args.width, args.height, args.frames, args.targets
+    W, H, T = args.width, args.height, args.targets
     ll = 2 * W
     fb = H * ll
     ranges = RANGES[:T]
-    frames = torch.empty(F * fb, dtype=torch.uint8, device=dev)
+    if args.total_frames:  # strong scaling: a fixed batch split over the ranks
+        total = args.total_frames
+        first, F = frame_shard(total, rank, world)
+    else:  # weak scaling: F frames per rank
+        F = args.frames
+        total = world * F
+        first, count = frame_shard(total, rank, world)
+        assert count == F
+    frames = torch.empty(max(F, 1) * fb, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
-    first, count = frame_shard(world * F, rank, world)  # weak scaling: F frames per rank
-    assert count == F
     trik_hsv.synth(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, args.kind, SEED, first_frame=first)
     det = trik_hsv.Detector(hot={"auto": trik_hsv.HOT_AUTO, "stripe": trik_hsv.HOT_STRIPE,
                                  "chroma": trik_hsv.HOT_CHROMA}[args.hot])
@@ -166,22 +193,29 @@ def main():
         if ev1 is not None:
             ev1.record(stream)
         targets = trik_hsv.batch_targets(sums, W, H, stream=stream)
-        all_reduce_totals(batch_totals(sums))  # RCCL over xGMI when N > 1: 3*T int64 per step
+        totals = batch_totals(sums)
+        if backend == "nccl":
+            all_reduce_totals(totals)  # RCCL over xGMI when N > 1: 3*T int64 per step
+        elif world > 1:  # gloo rehearsal: reduce a host copy
+            totals.copy_(all_reduce_totals(totals.cpu()))
         return targets
 
-    # cold batch: the first call with this range set compiles the range tables on
-    # the host, uploads them and builds the chroma-run tables on the device
-    # (stream-ordered, the host does not wait); timed apart from the steps
-    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    sums.zero_()
-    torch.cuda.synchronize()
-    c0.record(stream)
-    h0 = time.perf_counter()
-    det.batch_sums(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, ranges, sums, stream=stream)
-    host_call_ms = (time.perf_counter() - h0) * 1e3
-    c1.record(stream)
-    torch.cuda.synchronize()
-    cold_ms = c0.elapsed_time(c1)
+    def timed_call(rs):
+        """GPU time (HIP events on the stream) and host time of one batch_sums call."""
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        sums.zero_()
+        torch.cuda.synchronize()
+        c0.record(stream)
+        h0 = time.perf_counter()
+        det.batch_sums(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, rs, sums, stream=stream)
+        host_ms = (time.perf_counter() - h0) * 1e3
+        c1.record(stream)
+        torch.cuda.synchronize()
+        return c0.elapsed_time(c1), host_ms
+
+    # the first call of a fresh handle: table memory allocated, range tables
+    # compiled on the host and uploaded, chroma-run tables built on the device
+    first_ms, first_host_ms = timed_call(ranges)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -198,15 +232,29 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    # a range set the handle has not seen, on a warm handle (its table slots
+    # already allocated): what a workload that changes ranges pays per change.
+    # The host call only enqueues (no wait on the device).
+    def shifted(j):
+        return [(r[0] + j if k == 0 else r[0],) + tuple(r[1:]) for k, r in enumerate(ranges)]
+    for j in range(1, 5):  # fill the handle's table slots (4) with other sets
+        timed_call(shifted(j))
+    new_ms, new_host_ms = timed_call(shifted(5))
+    timed_call(ranges)  # back to the bench set (rebuilt)
     kname = {trik_hsv.HOT_CHROMA: "chroma_kernel", trik_hsv.HOT_STRIPE: "stripe_kernel",
              trik_hsv.HOT_GENERIC: "reduce_kernel"}.get(det.last_hot_kernel(), "?")
 
     el = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        if backend == "nccl":
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        else:
+            host = el.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.MAX)
+            el.copy_(host)
     elapsed, kern_ms_max = float(el[0]), float(el[1])
 
-    px_total = world * F * W * H * args.steps
+    px_total = total * W * H * args.steps
     value = px_total / elapsed / 1e6
     bytes_per_launch = F * fb  # algorithmic: 2 B/pixel read once
     achieved = bytes_per_launch / (kern_ms / 1e3) / 1e9
@@ -214,13 +262,12 @@ def main():
         "metric": METRIC, "value": round(value, 1), "unit": "Mpix/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "higher_is_better": True, "scaling": "strong" if args.total_frames else "weak", "vs_baseline": None,
+        "dtype": "u8",
         "data": "synthetic: device SplitMix64 uniform bytes, seed 0x7A1C" if args.kind == 0
                 else "synthetic: device scene generator (gradients + 6 discs), seed 0x7A1C",
-        "config": {"workload": f"C3: batch {F} x {W}x{H} YUYV per GPU, {T} HSV targets"
-                               + (f"; {F * world} frames over {world} GPUs" + (" (C5)" if world == 8 else "")
-                                  if world > 1 else ""),
-                   "frames_per_gpu": F, "width": W, "height": H, "line_length": ll,
+        "config": {"workload": workload_name(args.workload, F, total, world, W, H, T),
+                   "frames_per_gpu": F, "frames_total": total, "width": W, "height": H, "line_length": ll,
                    "targets": T, "layout": "yuyv", "parallelism": f"dp{world} (frame shards)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -228,11 +275,13 @@ def main():
                      "kernel": f"{kname}<YUYV,{T}>", "kernel_ms": round(kern_ms, 4),
                      "kernel_ms_max_rank": round(kern_ms_max, 4),
                      "bytes_per_launch": bytes_per_launch},
-        # first call with a new range set (not in `value`): tables compiled,
-        # uploaded and built on the device, then the hot kernel; the host call
-        # returns before that work runs
-        "cold_batch": {"cold_batch_ms": round(cold_ms, 4), "table_build_ms": round(cold_ms - kern_ms, 4),
-                       "host_call_ms": round(host_call_ms, 4)},
+        # a batch with a new range set (not in `value`)
+        "cold_batch": {"cold_batch_ms": round(new_ms, 4), "table_build_ms": round(new_ms - kern_ms, 4),
+                       "host_call_ms": round(new_host_ms, 4),
+                       "first_call_ms": round(first_ms, 4), "first_call_host_ms": round(first_host_ms, 4),
+                       "note": "cold_batch_ms: one batch with a range set new to a warm handle (tables "
+                               "compiled, uploaded and built on the device, then the hot kernel); "
+                               "first_call: a fresh handle, table memory allocated too"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb, parity = cpu_baseline(args, W, H, ll, T, sums.cpu().numpy())

@@ -12,6 +12,6 @@ rc=$?; echo "[q] bench rc=$rc"; tail -1 "$OUT/bench_$TAG.log" | python3 -c "impo
 ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run \
     -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline > "$OUT/prof_$TAG.log" 2>&1 )
 rc=$?; echo "[q] rocprof stats rc=$rc"; [ $rc -eq 0 ] || exit $rc
-grep -h stripe "$OUT/prof_$TAG/run_kernel_stats.csv" | cut -c1-40,150- || true
+grep -h "chroma_kernel\|stripe_kernel" "$OUT/prof_$TAG/run_kernel_stats.csv" | cut -d, -f1-4 | cut -c1-60,120- || true
 [ "${2:-}" = "--no-pmc" ] && exit 0
 bash scripts/pmc_session.sh "pmc_$TAG"
