@@ -494,6 +494,59 @@ int32_t trik_hsv_blob_preview(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvF
 int32_t trik_hsv_synth(const TrikHsvFrameBatch* batch, int32_t first_frame, int32_t kind,
                        uint64_t seed, void* hip_stream);
 
+/* ---------------------------------------------------------------------- */
+/* Layer 3: multi-GPU                                        */
+/* ---------------------------------------------------------------------- */
+/* Frames are independent units: a batch is sharded by frame index, each GPU
+ * processes its shard resident in its own memory, and the one exchange is the
+ * sum of the per-target batch totals (n_ranges x 3 int64) with one RCCL
+ * all-reduce over xGMI.  The reference has no multi-device path (one DSP, one
+ * frame per process call, WFXNS:174-264); these extend its batched surface.
+ * RCCL (librccl.so.1) is loaded on the first group/comm call. */
+
+/* Per-target batch totals on the device: totals_dev[r] = the sum over the
+ * n_frames frames of sums_dev[f][r] (each field), stream-ordered. */
+int32_t trik_hsv_batch_totals(int32_t n_frames, int32_t n_ranges, const TrikHsvTargetSums* sums_dev,
+                              TrikHsvTargetSums* totals_dev, void* hip_stream);
+
+/* One process driving several GPUs: per device an object-sensor handle
+ * (TRIK_VIDTRANSCODE_CV_create defaults), a HIP stream and a host worker
+ * thread, and an RCCL communicator over the devices (ncclCommInitAll). */
+typedef struct TrikHsvGroup* TRIK_HSV_GroupHandle;
+int32_t trik_hsv_group_create(int32_t n_devices, const int32_t* devices, TRIK_HSV_GroupHandle* out_group);
+/* Device d (0 <= d < n_devices) processes batches[d] -- its frames, in the
+ * memory of devices[d] -- as trik_hsv_process_batch does into sums_dev[d]
+ * ([n_frames][n_ranges]) and targets_dev[d] (may be NULL), then the per-target
+ * totals of its frames are summed over all devices with one ncclAllReduce
+ * into totals_dev[d] ([n_ranges], on devices[d]), so every device holds the
+ * totals of the whole batch.  Each device's worker thread enqueues its part on
+ * the device's stream; the call returns once every part is enqueued (see
+ * trik_hsv_group_sync).  A device with an empty shard (n_frames == 0) still
+ * takes part in the all-reduce. */
+int32_t trik_hsv_group_process(TRIK_HSV_GroupHandle group, const TrikHsvFrameBatch* batches,
+                               const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int32_t n_ranges,
+                               TrikHsvTargetSums* const* sums_dev, TrikHsvTarget* const* targets_dev,
+                               TrikHsvTargetSums* const* totals_dev);
+/* Waits for every device's enqueued work. */
+int32_t trik_hsv_group_sync(TRIK_HSV_GroupHandle group);
+/* The HIP stream device d's work runs on (for the caller's own ordering). */
+void* trik_hsv_group_stream(TRIK_HSV_GroupHandle group, int32_t d);
+int32_t trik_hsv_group_delete(TRIK_HSV_GroupHandle group);
+
+/* One process per GPU (the layout of torch.distributed / bench.py): an RCCL
+ * communicator over n_ranks processes, created on the calling thread's current
+ * device from an id that rank 0 makes (trik_hsv_comm_id) and the caller
+ * distributes to the other ranks by its own means. */
+#define TRIK_HSV_COMM_ID_BYTES 128
+typedef struct TrikHsvComm* TRIK_HSV_CommHandle;
+int32_t trik_hsv_comm_id(uint8_t id[TRIK_HSV_COMM_ID_BYTES]);
+int32_t trik_hsv_comm_create(int32_t n_ranks, int32_t rank, const uint8_t id[TRIK_HSV_COMM_ID_BYTES],
+                             TRIK_HSV_CommHandle* out_comm);
+/* In place, stream-ordered: totals_dev[n_ranges] summed over the ranks. */
+int32_t trik_hsv_comm_all_reduce_totals(TRIK_HSV_CommHandle comm, TrikHsvTargetSums* totals_dev,
+                                        int32_t n_ranges, void* hip_stream);
+int32_t trik_hsv_comm_delete(TRIK_HSV_CommHandle comm);
+
 #ifdef __cplusplus
 }
 #endif

@@ -30,6 +30,14 @@ int32_t fail(int32_t code, const std::string& msg) {
   return code;
 }
 
+}  // namespace
+
+// The last-error slot of the calling thread, for the other translation units
+// (trik_hsv_group.cpp reports its workers' errors on the caller's thread).
+int32_t trik_hsv::set_error(int32_t code, const std::string& msg) { return fail(code, msg); }
+
+namespace {
+
 #define HIP_TRY(expr)                                                                  \
   do {                                                                                 \
     hipError_t e_ = (hipError_t)(expr);                                                \
@@ -1170,6 +1178,15 @@ extern "C" int32_t trik_hsv_batch_sums(TRIK_VIDTRANSCODE_CV_Handle h, const Trik
   std::lock_guard<std::mutex> lock(h->mu);
   DeviceGuard dg(h->device);
   return run_sums(h, b, ranges, n, sums, nullptr, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int32_t trik_hsv_batch_totals(int32_t n_frames, int32_t n_ranges, const TrikHsvTargetSums* sums,
+                                         TrikHsvTargetSums* totals, void* stream) {
+  if (n_frames < 0 || n_ranges < 1 || n_ranges > TRIK_HSV_MAX_RANGES)
+    return fail(TRIK_IVIDTRANSCODE_EFAIL, "batch_totals: need n_frames >= 0 and n_ranges 1..64");
+  if (!totals || (n_frames > 0 && !sums)) return fail(TRIK_IVIDTRANSCODE_EFAIL, "batch_totals: NULL buffer");
+  HIP_TRY(launch_totals(n_frames, n_ranges, sums, totals, static_cast<hipStream_t>(stream)));
+  return 0;
 }
 
 extern "C" int32_t trik_hsv_batch_targets(const TrikHsvFrameBatch* b, int32_t n,

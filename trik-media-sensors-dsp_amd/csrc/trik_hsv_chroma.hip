@@ -87,8 +87,10 @@ static_assert(kLdsBlocks + 8192 <= kLdsPairs, "LDS layout");
 // The hot kernel keeps the block words as two byte tables in the same 8 KiB:
 // the pair's palette offset and the cut, both indexed by the block c >> 4
 // (one shift for both addresses; the offset byte is the pair's address).
+#if TRIK_CHROMA_SPLITB
 constexpr uint32_t kLdsBlkPair = kLdsBlocks;          // u8 [4096]
 constexpr uint32_t kLdsBlkCut = kLdsBlocks + 4096;    // u8 [4096]
+#endif
 constexpr uint32_t kLdsBytes = kLdsQueues + (kHotLanes / 64) * kHotQueueCap * 8;
 static_assert(kLdsBytes <= 160 * 1024, "chroma kernel LDS image");
 

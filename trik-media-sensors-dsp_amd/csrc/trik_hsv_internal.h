@@ -3,6 +3,8 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+
+#include <string>
 #include <stdint.h>
 
 #include "../../include/trik_hsv.h"
@@ -191,6 +193,10 @@ int launch_stripe(const KernelArgs& a, bool write_masks, hipStream_t s);
 int build_chroma_tables(const RangeTables* t, ChromaTables* ct, hipStream_t s);
 bool chroma_geometry_ok(const KernelArgs& a);
 int launch_chroma(const KernelArgs& a, const ChromaTables* ct, bool write_masks, hipStream_t s);
+// Sets the calling thread's trik_hsv_last_error() message; returns code.
+int32_t set_error(int32_t code, const std::string& msg);
+int launch_totals(int n_frames, int n_ranges, const TrikHsvTargetSums* sums, TrikHsvTargetSums* totals,
+                  hipStream_t s);
 int launch_targets(const TrikHsvFrameBatch& b, int n_ranges, const TrikHsvTargetSums* sums,
                    TrikHsvTarget* targets, hipStream_t s);
 int launch_synth(const TrikHsvFrameBatch& b, uint8_t* frames, int first_frame, int kind,

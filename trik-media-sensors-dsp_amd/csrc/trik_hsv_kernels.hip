@@ -347,6 +347,32 @@ int launch_targets(const TrikHsvFrameBatch& b, int n_ranges, const TrikHsvTarget
   return hipGetLastError();
 }
 
+// Per-target batch totals (the one value exchanged between
+// ranks): totals[r] = sum over frames of sums[f][r], field by field, int64.
+// One 256-lane workgroup per (range, field); the same order on every call.
+__global__ __launch_bounds__(256) void totals_kernel(int n_frames, int n_ranges, const TrikHsvTargetSums* sums,
+                                                     TrikHsvTargetSums* totals) {
+  const int r = blockIdx.x / 3, c = blockIdx.x % 3;
+  const long long* src = reinterpret_cast<const long long*>(sums) + (int64_t)r * 3 + c;
+  long long acc = 0;
+  for (int f = threadIdx.x; f < n_frames; f += blockDim.x) acc += src[(int64_t)f * n_ranges * 3];
+  __shared__ long long part[256];
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) reinterpret_cast<long long*>(totals)[(int64_t)r * 3 + c] = part[0];
+}
+
+int launch_totals(int n_frames, int n_ranges, const TrikHsvTargetSums* sums, TrikHsvTargetSums* totals,
+                  hipStream_t s) {
+  if (n_ranges <= 0) return hipSuccess;
+  hipLaunchKernelGGL(totals_kernel, dim3(3 * n_ranges), dim3(256), 0, s, n_frames, n_ranges, sums, totals);
+  return hipGetLastError();
+}
+
 int launch_synth(const TrikHsvFrameBatch& b, uint8_t* frames, int first_frame, int kind,
                  uint64_t seed, hipStream_t s) {
   const uint64_t smix = [&] {

@@ -309,6 +309,75 @@ def batch_targets(sums, width, height, *, stream=None):
     return targets
 
 
+def batch_totals_device(sums, *, stream=None):
+    """Per-target batch totals on the device (trik_hsv_batch_totals):
+    sums int64 [N,T,3] -> [T,3]."""
+    import torch
+
+    N, T = sums.shape[0], sums.shape[1]
+    totals = torch.empty((T, 3), dtype=torch.int64, device=sums.device)
+    rc = _lib.trik_hsv_batch_totals(N, T, C.c_void_p(sums.data_ptr()), C.c_void_p(totals.data_ptr()),
+                                    _stream_ptr(stream, sums))
+    if rc:
+        raise TrikHsvError(rc, "trik_hsv_batch_totals")
+    return totals
+
+
+class Group:
+    """One process driving several GPUs through the C ABI's group
+    (trik_hsv_group_*): a handle, a stream and a host worker thread per
+    device, and one RCCL all-reduce of the per-target totals."""
+
+    def __init__(self, devices):
+        self.devices = [int(d) for d in devices]
+        arr = (C.c_int32 * len(self.devices))(*self.devices)
+        h = C.c_void_p()
+        rc = _lib.trik_hsv_group_create(len(self.devices), arr, C.byref(h))
+        if rc:
+            raise TrikHsvError(rc, "trik_hsv_group_create")
+        self._h = h
+
+    def process(self, shards, width, height, line_length, layout, ranges):
+        """shards[d]: (frames tensor on devices[d], n_frames).  Returns per
+        device (sums [n,T,3], targets [n,T,4], totals [T,3]) -- enqueued on the
+        group's streams; call sync() before reading them."""
+        import torch
+
+        n = len(self.devices)
+        if len(shards) != n:
+            raise ValueError("one shard per device")
+        arr, T = _ranges(ranges)
+        batches = (_abi.FrameBatch * n)()
+        out, keep = [], []
+        for d, (frames, nf) in enumerate(shards):
+            dev = torch.device("cuda", self.devices[d])
+            batches[d] = _batch(frames, width, height, line_length, layout, nf)
+            sums = torch.zeros((max(nf, 0), T, 3), dtype=torch.int64, device=dev)
+            targets = torch.zeros((max(nf, 0), T, 4), dtype=torch.int8, device=dev)
+            totals = torch.zeros((T, 3), dtype=torch.int64, device=dev)
+            out.append((sums, targets, totals))
+        torch.cuda.synchronize()  # the allocations above ran on torch's streams
+        ptrs = [(C.c_void_p * n)(*[C.c_void_p(o[k].data_ptr()) for o in out]) for k in range(3)]
+        rc = _lib.trik_hsv_group_process(self._h, batches, arr, T, ptrs[0], ptrs[1], ptrs[2])
+        if rc:
+            raise TrikHsvError(rc, "trik_hsv_group_process")
+        self._keep = (batches, ptrs, out)
+        return out
+
+    def sync(self):
+        rc = _lib.trik_hsv_group_sync(self._h)
+        if rc:
+            raise TrikHsvError(rc, "trik_hsv_group_sync")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.trik_hsv_group_delete(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
 def synth(frames, width, height, line_length, layout, kind, seed, *, first_frame=0, n_frames=None,
           frame_stride=None, stream=None):
     """Fill a uint8 device tensor with synthetic frames (kind 0 uniform, 1 scene)."""

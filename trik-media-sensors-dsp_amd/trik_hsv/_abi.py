@@ -200,6 +200,18 @@ PROTOTYPES = {
     "trik_hsv_set_hot_kernel": ([C.c_void_p, i32], i32),
     "trik_hsv_last_hot_kernel": ([C.c_void_p], i32),
     "trik_hsv_chroma_share": ([C.c_void_p, C.POINTER(C.c_double)], i32),
+    # multi-GPU layer
+    "trik_hsv_batch_totals": ([i32, i32, C.c_void_p, C.c_void_p, C.c_void_p], i32),
+    "trik_hsv_group_create": ([i32, C.POINTER(i32), C.POINTER(C.c_void_p)], i32),
+    "trik_hsv_group_process": ([C.c_void_p, C.POINTER(FrameBatch), C.POINTER(InArgsAlg), i32,
+                                C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)], i32),
+    "trik_hsv_group_sync": ([C.c_void_p], i32),
+    "trik_hsv_group_stream": ([C.c_void_p, i32], C.c_void_p),
+    "trik_hsv_group_delete": ([C.c_void_p], i32),
+    "trik_hsv_comm_id": ([C.c_void_p], i32),
+    "trik_hsv_comm_create": ([i32, i32, C.c_void_p, C.POINTER(C.c_void_p)], i32),
+    "trik_hsv_comm_all_reduce_totals": ([C.c_void_p, C.c_void_p, i32, C.c_void_p], i32),
+    "trik_hsv_comm_delete": ([C.c_void_p], i32),
 }
 
 _lib = None
