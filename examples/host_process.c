@@ -2,7 +2,11 @@
  * host_process.c -- the reference's ARM-side call sequence (Codec Engine
  * VIDTRANSCODE_create / _control / _process / _delete on the object sensor,
  * trik/webcam/object_sensor/src/vidtranscode_cv_fxns.c) made against
- * libtrik_hsv.so in plain C, as INTEGRATION.md section 3 describes.
+ * libtrik_hsv.so in plain C, as INTEGRATION.md section 3 describes.  Like
+ * Codec Engine, it binds only the codec's function table
+ * (TRIK_VIDTRANSCODE_CV_FXNS, WFXNS:36-40): algAlloc -> allocate the memory
+ * records -> algInit -> control / process -> algFree -> release the records
+ * (ALG_create / ALG_delete of TI's framework, restated below).
  *
  * usage: host_process FRAME.yuyv WIDTH HEIGHT HUE_FROM HUE_TO SAT_FROM SAT_TO VAL_FROM VAL_TO
  * Reads one packed YUYV frame (lineLength = 2*WIDTH), prints
@@ -25,6 +29,38 @@ static uint32_t crc32(const uint8_t* p, size_t n) {
   return ~c;
 }
 
+#define MAX_RECS 16
+
+/* ALG_create: the codec's memory records allocated as it asks, the table in
+ * the object's first word, then algInit. */
+static TRIK_IALG_Handle alg_create(const TRIK_IVIDTRANSCODE_Fxns* fx, const TRIK_VIDTRANSCODE_CV_Params* params,
+                                   TRIK_IALG_MemRec* mem, int* n) {
+  TRIK_IALG_Fxns* parent = NULL;
+  *n = fx->ialg.algAlloc((const TRIK_IALG_Params*)params, &parent, mem);
+  if (*n < 1 || *n > MAX_RECS) return NULL;
+  for (int i = 0; i < *n; ++i) {
+    size_t align = mem[i].alignment > 16 ? (size_t)mem[i].alignment : 16;
+    size_t size = ((size_t)mem[i].size + align - 1) / align * align;
+    mem[i].base = aligned_alloc(align, size);
+    if (!mem[i].base) return NULL;
+    memset(mem[i].base, 0, size);
+  }
+  TRIK_IALG_Handle alg = (TRIK_IALG_Handle)mem[0].base;
+  alg->fxns = &fx->ialg;
+  if (fx->ialg.algInit(alg, mem, NULL, (const TRIK_IALG_Params*)params) != TRIK_IALG_EOK) {
+    for (int i = 0; i < *n; ++i) free(mem[i].base);
+    return NULL;
+  }
+  return alg;
+}
+
+/* ALG_delete: algFree hands back the records, which are released. */
+static void alg_delete(const TRIK_IVIDTRANSCODE_Fxns* fx, TRIK_IALG_Handle alg) {
+  TRIK_IALG_MemRec mem[MAX_RECS];
+  const int n = fx->ialg.algFree(alg, mem);
+  for (int i = 0; i < n && i < MAX_RECS; ++i) free(mem[i].base);
+}
+
 int main(int argc, char** argv) {
   if (argc != 10) {
     fprintf(stderr, "usage: %s FRAME W H hueFrom hueTo satFrom satTo valFrom valTo\n", argv[0]);
@@ -40,8 +76,11 @@ int main(int argc, char** argv) {
   }
   fclose(f);
 
-  TRIK_VIDTRANSCODE_CV_Handle hd;
-  if (TRIK_VIDTRANSCODE_CV_create(NULL, &hd) != TRIK_IALG_EOK) {  /* VIDTRANSCODE_create */
+  const TRIK_IVIDTRANSCODE_Fxns* fx = &TRIK_VIDTRANSCODE_CV_FXNS;
+  TRIK_IALG_MemRec mem[MAX_RECS];
+  int n_recs = 0;
+  TRIK_IALG_Handle hd = alg_create(fx, NULL, mem, &n_recs);  /* VIDTRANSCODE_create */
+  if (!hd) {
     fprintf(stderr, "create: %s\n", trik_hsv_last_error());
     return 3;
   }
@@ -57,7 +96,7 @@ int main(int argc, char** argv) {
   TRIK_IVIDTRANSCODE_Status st;
   memset(&st, 0, sizeof st);
   st.size = sizeof st;
-  if (TRIK_VIDTRANSCODE_CV_control(hd, TRIK_XDM_SETPARAMS, &dyn, &st) != TRIK_IALG_EOK) {  /* _control */
+  if (fx->control(hd, TRIK_XDM_SETPARAMS, &dyn, &st) != TRIK_IALG_EOK) {  /* _control */
     fprintf(stderr, "control: %s\n", trik_hsv_last_error());
     return 3;
   }
@@ -84,10 +123,11 @@ int main(int argc, char** argv) {
   TRIK_VIDTRANSCODE_CV_OutArgs oa;
   memset(&oa, 0, sizeof oa);
   oa.base.size = sizeof oa;
-  const int32_t rc = TRIK_VIDTRANSCODE_CV_process(hd, &in, &out, &ia, &oa);  /* _process */
+  const int32_t rc = fx->process(hd, &in, &out, (TRIK_IVIDTRANSCODE_InArgs*)&ia,
+                                 (TRIK_IVIDTRANSCODE_OutArgs*)&oa);  /* _process */
   printf("%d %d %d %u %08x\n", rc, oa.alg.targetX, oa.alg.targetY, oa.alg.targetSize,
          crc32(preview, preview_bytes));
-  TRIK_VIDTRANSCODE_CV_delete(hd);  /* VIDTRANSCODE_delete */
+  alg_delete(fx, hd);  /* VIDTRANSCODE_delete */
   free(preview);
   free(frame);
   return rc == TRIK_IVIDTRANSCODE_EOK ? 0 : 1;

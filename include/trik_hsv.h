@@ -327,6 +327,86 @@ int32_t TRIK_VIDTRANSCODE_CV_control(TRIK_VIDTRANSCODE_CV_Handle handle, int32_t
                                      TRIK_IVIDTRANSCODE_Status* status);
 
 /* ---------------------------------------------------------------------- */
+/* Layer 1b: the XDAIS function tables (WFXNS:20-66, 85-166)               */
+/* ---------------------------------------------------------------------- */
+/* What a Codec-Engine-style framework binds: IALG_Fxns + IVIDTRANSCODE_Fxns,
+ * restated from TI XDAIS ialg.h / ividtranscode.h (absent here; Int/Uns are
+ * 32-bit on the C64x+, so int32_t/uint32_t).  The framework calls algAlloc
+ * for the memory records, allocates them, stores the table in the object's
+ * first word (IALG_Obj.fxns), calls algInit, then process/control through
+ * the table, then algFree and releases the records.  The object IS a
+ * TRIK_VIDTRANSCODE_CV_Handle: the table's process/control are the quartet's
+ * process/control, and TRIK_VIDTRANSCODE_CV_create/_delete are the same
+ * alloc + init / free with the library owning the memory. */
+typedef enum TRIK_IALG_MemAttrs { TRIK_IALG_SCRATCH = 0, TRIK_IALG_PERSIST = 1, TRIK_IALG_WRITEONCE = 2 } TRIK_IALG_MemAttrs;
+#define TRIK_IALG_MXTRN 0x0010 /* ialg.h: external memory space bit */
+#define TRIK_IALG_DARAM0 0
+#define TRIK_IALG_EXTERNAL (TRIK_IALG_MXTRN + 1)
+
+typedef struct TRIK_IALG_MemRec {
+  uint32_t size;      /* Uns */
+  int32_t alignment;  /* Int: 0 = any */
+  int32_t space;      /* IALG_MemSpace */
+  int32_t attrs;      /* IALG_MemAttrs */
+  void* base;
+} TRIK_IALG_MemRec;
+
+struct TRIK_IALG_Fxns;
+typedef struct TRIK_IALG_Obj {
+  const struct TRIK_IALG_Fxns* fxns;
+} TRIK_IALG_Obj;
+typedef TRIK_IALG_Obj* TRIK_IALG_Handle;
+
+/* IALG_Params: the codec's TRIK_VIDTRANSCODE_CV_Params (its first field is the size). */
+typedef struct TRIK_IALG_Params {
+  int32_t size;
+} TRIK_IALG_Params;
+
+typedef struct TRIK_IALG_Fxns {
+  const void* implementationId;
+  void (*algActivate)(TRIK_IALG_Handle);
+  int32_t (*algAlloc)(const TRIK_IALG_Params*, struct TRIK_IALG_Fxns**, TRIK_IALG_MemRec*);
+  int32_t (*algControl)(TRIK_IALG_Handle, int32_t, void*);
+  void (*algDeactivate)(TRIK_IALG_Handle);
+  int32_t (*algFree)(TRIK_IALG_Handle, TRIK_IALG_MemRec*);
+  int32_t (*algInit)(TRIK_IALG_Handle, const TRIK_IALG_MemRec*, TRIK_IALG_Handle, const TRIK_IALG_Params*);
+  void (*algMoved)(TRIK_IALG_Handle, const TRIK_IALG_MemRec*, TRIK_IALG_Handle, const TRIK_IALG_Params*);
+  int32_t (*algNumAlloc)(void);
+} TRIK_IALG_Fxns;
+
+/* IVIDTRANSCODE_Fxns.  in_args / out_args: the codec's InArgs / OutArgs
+ * (size fields checked), as IVIDTRANSCODE_InArgs* / _OutArgs* in TI's. */
+typedef struct TRIK_IVIDTRANSCODE_Fxns {
+  TRIK_IALG_Fxns ialg;
+  int32_t (*process)(TRIK_IALG_Handle, TRIK_XDM1_BufDesc*, TRIK_XDM_BufDesc*, TRIK_IVIDTRANSCODE_InArgs*,
+                     TRIK_IVIDTRANSCODE_OutArgs*);
+  int32_t (*control)(TRIK_IALG_Handle, int32_t, TRIK_VIDTRANSCODE_CV_DynamicParams*, TRIK_IVIDTRANSCODE_Status*);
+} TRIK_IVIDTRANSCODE_Fxns;
+
+/* The webcam object sensor's tables (WFXNS:36-66); IALG is the same table
+ * as FXNS.ialg (the reference aliases the two symbols on TI toolchains and
+ * duplicates them elsewhere, as here).  The other two codecs of this library
+ * (one DSP server each in the reference, all named TRIK_VIDTRANSCODE_CV_FXNS
+ * there): the ov7670 object sensor and the ov7670 line sensor. */
+extern TRIK_IVIDTRANSCODE_Fxns TRIK_VIDTRANSCODE_CV_FXNS;
+extern TRIK_IALG_Fxns TRIK_VIDTRANSCODE_CV_IALG;
+extern TRIK_IVIDTRANSCODE_Fxns TRIK_VIDTRANSCODE_CV_OV7670_FXNS;
+extern TRIK_IVIDTRANSCODE_Fxns TRIK_VIDTRANSCODE_CV_LINE_FXNS;
+
+/* The webcam object sensor's IALG functions (WFXNS:85-166), also reachable
+ * through the tables.  alloc asks for one persistent external record (the
+ * object; the reference's second record is C64x+ on-chip fast RAM, which
+ * has no use here) and returns the record count; initObj constructs the
+ * object in that record (keeping the framework's fxns word) and runs the
+ * setup of WFXNS:146-166; free destroys it and returns the record for the
+ * framework to release. */
+int32_t TRIK_VIDTRANSCODE_CV_alloc(const TRIK_IALG_Params* params, TRIK_IALG_Fxns** parent_fxns,
+                                   TRIK_IALG_MemRec mem_tab[]);
+int32_t TRIK_VIDTRANSCODE_CV_initObj(TRIK_IALG_Handle handle, const TRIK_IALG_MemRec mem_tab[],
+                                     TRIK_IALG_Handle parent, const TRIK_IALG_Params* params);
+int32_t TRIK_VIDTRANSCODE_CV_free(TRIK_IALG_Handle handle, TRIK_IALG_MemRec mem_tab[]);
+
+/* ---------------------------------------------------------------------- */
 /* Layer 2: batched device API                                             */
 /* ---------------------------------------------------------------------- */
 

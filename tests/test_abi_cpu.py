@@ -90,3 +90,42 @@ def test_header_compiles_as_cxx():
         open(c, "w").write('#include "trik_hsv.h"\nint main(){return TRIK_IALG_EOK;}\n')
         subprocess.run(["g++", "-std=c++11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
                         c, "-o", os.path.join(d, "h")], check=True)
+
+
+XDAIS_PROG = r"""
+#include <stdio.h>
+#include <stdlib.h>
+#include "trik_hsv.h"
+/* a Codec-Engine-style caller that binds only the function tables */
+int main(void) {
+  const TRIK_IVIDTRANSCODE_Fxns* tabs[3] = {&TRIK_VIDTRANSCODE_CV_FXNS, &TRIK_VIDTRANSCODE_CV_OV7670_FXNS,
+                                            &TRIK_VIDTRANSCODE_CV_LINE_FXNS};
+  for (int i = 0; i < 3; ++i) {
+    const TRIK_IVIDTRANSCODE_Fxns* f = tabs[i];
+    TRIK_IALG_MemRec m[16];
+    TRIK_IALG_Fxns* parent = NULL;
+    int n = f->ialg.algAlloc(NULL, &parent, m);
+    if (n != 1 || m[0].size < sizeof(TRIK_IALG_Obj) || m[0].attrs != TRIK_IALG_PERSIST) return 10 + i;
+    if (f->ialg.implementationId != (const void*)f || !f->process || !f->control || !f->ialg.algInit ||
+        !f->ialg.algFree || f->ialg.algActivate || f->ialg.algNumAlloc) return 20 + i;
+    printf("%d %u %d\n", n, m[0].size, m[0].alignment);
+  }
+  if (TRIK_VIDTRANSCODE_CV_IALG.algAlloc != TRIK_VIDTRANSCODE_CV_FXNS.ialg.algAlloc ||
+      TRIK_VIDTRANSCODE_CV_IALG.implementationId != (const void*)&TRIK_VIDTRANSCODE_CV_FXNS) return 30;
+  return 0;
+}
+"""
+
+
+def test_xdais_tables_link_from_c_and_alloc_without_gpu():
+    """The exported XDAIS tables (WFXNS:20-66) bind from plain C; algAlloc
+    needs no device."""
+    lib_dir = os.path.join(ROOT, "trik-media-sensors-dsp_amd", "trik_hsv")
+    with tempfile.TemporaryDirectory() as d:
+        c, exe = os.path.join(d, "x.c"), os.path.join(d, "x")
+        open(c, "w").write(XDAIS_PROG)
+        subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", f"-I{os.path.join(ROOT, 'include')}", c,
+                        f"-L{lib_dir}", "-ltrik_hsv", f"-Wl,-rpath,{lib_dir}", "-o", exe], check=True)
+        r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
+    assert len(r.stdout.split("\n")) >= 3

@@ -227,6 +227,11 @@ struct TableSet {
 constexpr int kTableSets = 4;
 
 struct TrikCvHandle {
+  // XDAIS IALG_Obj: the framework's function table (algInit keeps it)
+  TRIK_IALG_Obj ialg{};
+  // false when the object lives in a framework-allocated IALG record
+  // (algAlloc / algInit / algFree), true for TRIK_VIDTRANSCODE_CV_create
+  bool owns_memory = true;
   int device = 0;
   int algo = kAlgoBall;
   // line sensor: the cross-point rows the previous run left (LSEQ:298 reads
@@ -308,7 +313,10 @@ void release(TrikCvHandle* h) {
   (void)hipFree(h->d_blob_targets);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   if (switched) (void)hipSetDevice(prev);
-  delete h;
+  if (h->owns_memory)
+    delete h;
+  else
+    h->~TrikCvHandle();  // the framework releases the record (algFree)
 }
 
 // handleSetupImageDesc + createCVAlgorithm + BallDetector::setup
@@ -760,14 +768,19 @@ AutoRangeArgs auto_range_args(const TrikHsvFrameBatch& b, uint16_t* out) {
 // ---------------------------------------------------------------------------
 // Layer 1: XDAIS-shaped quartet
 // ---------------------------------------------------------------------------
-static int32_t create_handle(int algo, const TRIK_VIDTRANSCODE_CV_Params* params,
-                             TRIK_VIDTRANSCODE_CV_Handle* out_handle) {
-  if (!out_handle) return fail(TRIK_IALG_EFAIL, "out_handle is NULL");
-  *out_handle = nullptr;
-  TrikCvHandle* h = new (std::nothrow) TrikCvHandle();
-  if (!h) return fail(TRIK_IALG_EFAIL, "out of memory");
+extern "C" TRIK_IVIDTRANSCODE_Fxns TRIK_VIDTRANSCODE_CV_FXNS, TRIK_VIDTRANSCODE_CV_OV7670_FXNS,
+    TRIK_VIDTRANSCODE_CV_LINE_FXNS;
+
+static const TRIK_IALG_Fxns* table_of(int algo) {
+  return algo == kAlgoLine ? &TRIK_VIDTRANSCODE_CV_LINE_FXNS.ialg
+                           : (algo == kAlgoBlob ? &TRIK_VIDTRANSCODE_CV_OV7670_FXNS.ialg : &TRIK_VIDTRANSCODE_CV_FXNS.ialg);
+}
+
+// trikCvHandleInit + SetupParams + SetupDynamicParams (WFXNS:146-166) on a
+// constructed object; releases it on failure.
+static int32_t init_handle(TrikCvHandle* h, int algo, const TRIK_VIDTRANSCODE_CV_Params* params) {
   if (hipGetDevice(&h->device) != hipSuccess) {
-    delete h;
+    release(h);
     return fail(TRIK_IALG_EFAIL, "no HIP device");
   }
   h->algo = algo;
@@ -779,8 +792,19 @@ static int32_t create_handle(int algo, const TRIK_VIDTRANSCODE_CV_Params* params
     release(h);
     return rc;
   }
-  *out_handle = h;
   return TRIK_IALG_EOK;
+}
+
+static int32_t create_handle(int algo, const TRIK_VIDTRANSCODE_CV_Params* params,
+                             TRIK_VIDTRANSCODE_CV_Handle* out_handle) {
+  if (!out_handle) return fail(TRIK_IALG_EFAIL, "out_handle is NULL");
+  *out_handle = nullptr;
+  TrikCvHandle* h = new (std::nothrow) TrikCvHandle();
+  if (!h) return fail(TRIK_IALG_EFAIL, "out of memory");
+  h->ialg.fxns = table_of(algo);
+  const int32_t rc = init_handle(h, algo, params);
+  if (rc == TRIK_IALG_EOK) *out_handle = h;
+  return rc;
 }
 
 extern "C" int32_t TRIK_VIDTRANSCODE_CV_create(const TRIK_VIDTRANSCODE_CV_Params* params,
@@ -848,6 +872,101 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_control(TRIK_VIDTRANSCODE_CV_Handle h, i
       rc = fail(TRIK_IVIDTRANSCODE_EFAIL, "unsupported control command");
   }
   return rc;
+}
+
+// ---------------------------------------------------------------------------
+// Layer 1b: the XDAIS IALG functions and function tables (WFXNS:20-166)
+// ---------------------------------------------------------------------------
+// algAlloc: one persistent external record for the object (the reference's
+// second record, C64x+ on-chip fast RAM, has no use here)
+static int32_t ialg_alloc(const TRIK_IALG_Params*, TRIK_IALG_Fxns**, TRIK_IALG_MemRec mem_tab[]) {
+  if (!mem_tab) return fail(TRIK_IALG_EFAIL, "algAlloc: mem_tab is NULL");
+  mem_tab[0].size = (uint32_t)sizeof(TrikCvHandle);
+  mem_tab[0].alignment = (int32_t)alignof(TrikCvHandle);
+  mem_tab[0].space = TRIK_IALG_EXTERNAL;
+  mem_tab[0].attrs = TRIK_IALG_PERSIST;
+  mem_tab[0].base = nullptr;
+  return 1;
+}
+
+// algInit: the object is constructed in the framework's record; the fxns
+// word the framework stored there is kept
+static int32_t ialg_init(int algo, TRIK_IALG_Handle alg, const TRIK_IALG_MemRec mem_tab[], const TRIK_IALG_Params* params) {
+  if (!alg || !mem_tab || mem_tab[0].base != (void*)alg)
+    return fail(TRIK_IALG_EFAIL, "algInit: the handle must be mem_tab[0].base");
+  if (mem_tab[0].size < sizeof(TrikCvHandle) || (reinterpret_cast<uintptr_t>(alg) % alignof(TrikCvHandle)))
+    return fail(TRIK_IALG_EFAIL, "algInit: mem_tab[0] smaller or less aligned than algAlloc asked");
+  if (params && params->size != (int32_t)sizeof(TRIK_VIDTRANSCODE_CV_Params))
+    return fail(TRIK_IALG_EFAIL, "algInit: params size mismatch");
+  const TRIK_IALG_Fxns* fxns = alg->fxns;
+  TrikCvHandle* h = new (alg) TrikCvHandle();
+  h->ialg.fxns = fxns ? fxns : table_of(algo);
+  h->owns_memory = false;
+  return init_handle(h, algo, reinterpret_cast<const TRIK_VIDTRANSCODE_CV_Params*>(params));
+}
+
+static int32_t ialg_init_ball(TRIK_IALG_Handle a, const TRIK_IALG_MemRec* m, TRIK_IALG_Handle, const TRIK_IALG_Params* p) {
+  return ialg_init(kAlgoBall, a, m, p);
+}
+static int32_t ialg_init_blob(TRIK_IALG_Handle a, const TRIK_IALG_MemRec* m, TRIK_IALG_Handle, const TRIK_IALG_Params* p) {
+  return ialg_init(kAlgoBlob, a, m, p);
+}
+static int32_t ialg_init_line(TRIK_IALG_Handle a, const TRIK_IALG_MemRec* m, TRIK_IALG_Handle, const TRIK_IALG_Params* p) {
+  return ialg_init(kAlgoLine, a, m, p);
+}
+
+// algFree: the object is destroyed; its record is returned for the framework
+static int32_t ialg_free(TRIK_IALG_Handle alg, TRIK_IALG_MemRec mem_tab[]) {
+  if (!alg || !mem_tab) return fail(TRIK_IALG_EFAIL, "algFree: NULL argument");
+  TrikCvHandle* h = reinterpret_cast<TrikCvHandle*>(alg);
+  if (h->owns_memory) return fail(TRIK_IALG_EFAIL, "algFree: handle made by TRIK_VIDTRANSCODE_CV_create");
+  release(h);
+  mem_tab[0].base = alg;
+  mem_tab[0].size = (uint32_t)sizeof(TrikCvHandle);
+  mem_tab[0].alignment = (int32_t)alignof(TrikCvHandle);
+  mem_tab[0].space = TRIK_IALG_EXTERNAL;
+  mem_tab[0].attrs = TRIK_IALG_PERSIST;
+  return 1;
+}
+
+static int32_t xdais_process(TRIK_IALG_Handle alg, TRIK_XDM1_BufDesc* in, TRIK_XDM_BufDesc* out,
+                             TRIK_IVIDTRANSCODE_InArgs* in_args, TRIK_IVIDTRANSCODE_OutArgs* out_args) {
+  return TRIK_VIDTRANSCODE_CV_process(reinterpret_cast<TRIK_VIDTRANSCODE_CV_Handle>(alg), in, out,
+                                      reinterpret_cast<TRIK_VIDTRANSCODE_CV_InArgs*>(in_args),
+                                      reinterpret_cast<TRIK_VIDTRANSCODE_CV_OutArgs*>(out_args));
+}
+
+static int32_t xdais_control(TRIK_IALG_Handle alg, int32_t cmd, TRIK_VIDTRANSCODE_CV_DynamicParams* dyn,
+                             TRIK_IVIDTRANSCODE_Status* status) {
+  return TRIK_VIDTRANSCODE_CV_control(reinterpret_cast<TRIK_VIDTRANSCODE_CV_Handle>(alg), cmd, dyn, status);
+}
+
+// WFXNS:20-29: module ID, activate, alloc, control, deactivate, free, init,
+// moved, numAlloc (NULL => IALG_MAXMEMRECS)
+#define TRIK_IALGFXNS(self, init) {&self, nullptr, ialg_alloc, nullptr, nullptr, ialg_free, init, nullptr, nullptr}
+
+extern "C" {
+TRIK_IVIDTRANSCODE_Fxns TRIK_VIDTRANSCODE_CV_FXNS = {TRIK_IALGFXNS(TRIK_VIDTRANSCODE_CV_FXNS, ialg_init_ball),
+                                                     xdais_process, xdais_control};
+TRIK_IALG_Fxns TRIK_VIDTRANSCODE_CV_IALG = TRIK_IALGFXNS(TRIK_VIDTRANSCODE_CV_FXNS, ialg_init_ball);
+TRIK_IVIDTRANSCODE_Fxns TRIK_VIDTRANSCODE_CV_OV7670_FXNS = {
+    TRIK_IALGFXNS(TRIK_VIDTRANSCODE_CV_OV7670_FXNS, ialg_init_blob), xdais_process, xdais_control};
+TRIK_IVIDTRANSCODE_Fxns TRIK_VIDTRANSCODE_CV_LINE_FXNS = {TRIK_IALGFXNS(TRIK_VIDTRANSCODE_CV_LINE_FXNS, ialg_init_line),
+                                                          xdais_process, xdais_control};
+}
+
+extern "C" int32_t TRIK_VIDTRANSCODE_CV_alloc(const TRIK_IALG_Params* params, TRIK_IALG_Fxns** parent_fxns,
+                                              TRIK_IALG_MemRec mem_tab[]) {
+  return ialg_alloc(params, parent_fxns, mem_tab);
+}
+
+extern "C" int32_t TRIK_VIDTRANSCODE_CV_initObj(TRIK_IALG_Handle alg, const TRIK_IALG_MemRec mem_tab[],
+                                                TRIK_IALG_Handle parent, const TRIK_IALG_Params* params) {
+  return ialg_init_ball(alg, mem_tab, parent, params);
+}
+
+extern "C" int32_t TRIK_VIDTRANSCODE_CV_free(TRIK_IALG_Handle alg, TRIK_IALG_MemRec mem_tab[]) {
+  return ialg_free(alg, mem_tab);
 }
 
 extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,

@@ -200,6 +200,10 @@ PROTOTYPES = {
     "trik_hsv_set_hot_kernel": ([C.c_void_p, i32], i32),
     "trik_hsv_last_hot_kernel": ([C.c_void_p], i32),
     "trik_hsv_chroma_share": ([C.c_void_p, C.POINTER(C.c_double)], i32),
+    # XDAIS IALG functions (also in the exported function tables)
+    "TRIK_VIDTRANSCODE_CV_alloc": ([C.c_void_p, C.c_void_p, C.c_void_p], i32),
+    "TRIK_VIDTRANSCODE_CV_initObj": ([C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], i32),
+    "TRIK_VIDTRANSCODE_CV_free": ([C.c_void_p, C.c_void_p], i32),
     # multi-GPU layer
     "trik_hsv_batch_totals": ([i32, i32, C.c_void_p, C.c_void_p, C.c_void_p], i32),
     "trik_hsv_group_create": ([i32, C.POINTER(i32), C.POINTER(C.c_void_p)], i32),
