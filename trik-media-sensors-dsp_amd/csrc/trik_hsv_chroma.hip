@@ -68,8 +68,13 @@ constexpr int kQueueCap = 128;  // blob kernel, entries per wave: < 64 waiting +
 // queue down to < kDrainAt entries after every step, and a step appends its
 // words at once when they fit (else word by word, draining before each).
 constexpr int kHotLanes = 960;
-constexpr int kDrainAt = 60;
-constexpr int kHotQueueCap = kDrainAt - 1 + 128;
+constexpr int kHotQueueCap = 59 + 128;  // what the LDS image leaves: 15 x 187 x 8 B
+// per-step appends drain full rounds of 64; word-by-word appends (A/B) drain at
+// 60 every second word, so the queue holds < 60 + 128 entries
+#ifndef TRIK_CHROMA_DRAIN_AT
+#define TRIK_CHROMA_DRAIN_AT 64
+#endif
+constexpr int kDrainAt = TRIK_CHROMA_Q2 ? TRIK_CHROMA_DRAIN_AT : 60;
 
 // LDS image of the chroma kernel (dynamic LDS from address 0).  The block
 // masks and the mask-pair table sit below 64 KiB so their reads take an
@@ -187,27 +192,35 @@ __device__ __forceinline__ uint32_t chroma_of(uint32_t w) { return __builtin_amd
 //   bits 0-1 number of runs (3 = more than two), 4-7 v1, 8-11 v2,
 //   12-20 end of run 1, 21-29 end of run 2 (two runs) or of the last nonzero
 //   run (more than two).
+// One workgroup per (V, quarter of the U range): 256 threads evaluate the
+// 64 chromas' masks for a quarter of the Y range each into LDS, then one
+// thread per chroma walks its 256 masks.
 __global__ __launch_bounds__(256) void chroma_summary_kernel(const RangeTables* t, ChromaTables* ct) {
-  const int U = threadIdx.x, V = blockIdx.x;
+  __shared__ uint8_t prof[64][256 + 4];  // [chroma][Y], rows padded against bank conflicts
+  const int V = blockIdx.x >> 2, U0 = (blockIdx.x & 3) * 64;
+  {
+    const int u = threadIdx.x & 63, y0 = (threadIdx.x >> 6) * 64;
+    for (int y = y0; y < y0 + 64; ++y) prof[u][y] = (uint8_t)detect_pixel(y, U0 + u, V, *t);
+  }
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  const int U = U0 + (int)threadIdx.x;
+  const uint8_t* row = prof[threadIdx.x];
   const uint32_t c = (uint32_t)U | ((uint32_t)V << 8);
   int nruns = 0;            // runs so far, including the current one
   uint32_t vals[3] = {0, 0, 0};
   int ends[3] = {0, 0, 0};  // exclusive end of each run
   uint32_t cur = 0xFFu;
   int last_nz_run = -1, last_nz_end = 0;
-  for (int y4 = 0; y4 < 256; y4 += 4) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int Y = y4 + j;
-      const uint32_t m = detect_pixel(Y, U, V, *t);
-      if (m != cur) {
-        if (nruns < 3) vals[nruns] = m;
-        ++nruns;
-        cur = m;
-      }
-      if (nruns <= 3) ends[nruns - 1] = Y + 1;
-      if (m) { last_nz_run = nruns - 1; last_nz_end = Y + 1; }
+  for (int Y = 0; Y < 256; ++Y) {
+    const uint32_t m = row[Y];
+    if (m != cur) {
+      if (nruns < 3) vals[nruns] = m;
+      ++nruns;
+      cur = m;
     }
+    if (nruns <= 3) ends[nruns - 1] = Y + 1;
+    if (m) { last_nz_run = nruns - 1; last_nz_end = Y + 1; }
   }
   // runs up to and including the last nonzero one
   const int n = last_nz_run + 1;  // 0: all zero
@@ -274,61 +287,81 @@ __device__ __forceinline__ uint32_t chroma_desc_cut(uint32_t sf, uint32_t sd, ui
   return chroma_desc(f == A ? sd : sf, k & 15u, k >> 4);
 }
 
-// One workgroup per 16-chroma block b = (V << 4) | (U >> 4), one thread per
-// mask pair k = M1 | M2 << 4: each thread finds the cut A (0, or the first
-// nonzero Y of one of the block's chromas) with the fewest expected
-// exact-path words over the block, and the workgroup keeps the cheapest
-// (cost, k, A) (ties: smaller k, then smaller A).  PALETTE = false: all pairs
-// whose masks occur in the block; the choice is counted in pair_hist.
-// PALETTE = true: the palette's pairs only (the same choice when the
-// unrestricted pair made the palette, which is nearly always); then the block
-// byte (the pair's palette offset), the cut and the run descriptors.
+// One workgroup per 16-chroma block b = (V << 4) | (U >> 4): the candidate
+// mask pairs k = M1 | M2 << 4 and cuts A (0, or the first nonzero Y of one of
+// the block's chromas) are listed in LDS and their combinations spread over
+// the 256 threads; the workgroup keeps the (cost, k, A) with the fewest
+// expected exact-path words over the block (ties: smaller k, then smaller A).
+// PALETTE = false: all pairs whose masks occur in the block; the choice is
+// counted in pair_hist.  PALETTE = true: the palette's pairs only (the same
+// choice when the unrestricted pair made the palette, which is nearly
+// always); then the block word (the pair's palette offset | the cut << 8)
+// and the run descriptors.
 template <bool PALETTE>
 __global__ __launch_bounds__(256) void chroma_block_kernel(ChromaTables* ct) {
   __shared__ uint32_t sf[16], sd[16], fz[16];
+  __shared__ uint32_t pairs[256], cuts[17];
+  __shared__ uint32_t n_pairs, n_cuts;
   __shared__ unsigned long long best;
   const int b = blockIdx.x;
-  const uint32_t k = threadIdx.x;
+  const uint32_t t = threadIdx.x;
   const uint32_t c0 = ((uint32_t)(b >> 4) << 8) | ((uint32_t)(b & 15) << 4);
-  if (k < 16) {
-    sf[k] = ct->summary[c0 + k];
-    sd[k] = ct->summary_drop[c0 + k];
-    fz[k] = ct->first_nz[c0 + k];
+  if (t < 16) {
+    sf[t] = ct->summary[c0 + t];
+    sd[t] = ct->summary_drop[c0 + t];
+    fz[t] = ct->first_nz[c0 + t];
   }
-  if (k == 0) best = ~0ull;
+  if (t == 0) {
+    best = ~0ull;
+    n_pairs = 0;
+  }
   __syncthreads();
-  uint32_t present = 1u;  // mask values appearing (value 0 always a candidate)
-  for (int i = 0; i < 16; ++i) {
-    if (sf[i] & 3u) present |= 1u << ((sf[i] >> 4) & 15u);
-    if ((sf[i] & 3u) == 2u) present |= 1u << ((sf[i] >> 8) & 15u);
-    if (sd[i] & 3u) present |= 1u << ((sd[i] >> 4) & 15u);
-    if ((sd[i] & 3u) == 2u) present |= 1u << ((sd[i] >> 8) & 15u);
+  if (t == 0) {  // the cuts: 0, then each chroma's first nonzero Y in (0, 255]
+    uint32_t n = 0;
+    cuts[n++] = 0;
+    for (int j = 0; j < 16; ++j)
+      if (fz[j] != 0u && fz[j] <= 255u) cuts[n++] = fz[j];
+    n_cuts = n;
   }
-  const bool skip = PALETTE ? ct->palette_of[k] == 0xFFu
-                            : (!((present >> (k & 15u)) & 1u) || !((present >> (k >> 4)) & 1u));
-  if (!skip) {
-    unsigned long long mine = ~0ull;
-    for (int j = -1; j < 16; ++j) {
-      const uint32_t A = j < 0 ? 0u : fz[j];
-      if (j >= 0 && (A == 0u || A > 255u)) continue;
-      uint32_t cost = 0;
-      for (int i = 0; i < 16; ++i) cost += chroma_cost(chroma_desc_cut(sf[i], sd[i], fz[i], k, A));
-      const unsigned long long key = ((unsigned long long)cost << 17) | ((unsigned long long)k << 9) | A;
-      if (key < mine) mine = key;
+  {  // the pairs: thread t stands for pair k = t
+    const uint32_t k = t;
+    bool take;
+    if (PALETTE) {
+      take = ct->palette_of[k] != 0xFFu;
+    } else {
+      uint32_t present = 1u;  // mask values appearing (value 0 always a candidate)
+      for (int i = 0; i < 16; ++i) {
+        if (sf[i] & 3u) present |= 1u << ((sf[i] >> 4) & 15u);
+        if ((sf[i] & 3u) == 2u) present |= 1u << ((sf[i] >> 8) & 15u);
+        if (sd[i] & 3u) present |= 1u << ((sd[i] >> 4) & 15u);
+        if ((sd[i] & 3u) == 2u) present |= 1u << ((sd[i] >> 8) & 15u);
+      }
+      take = ((present >> (k & 15u)) & 1u) && ((present >> (k >> 4)) & 1u);
     }
-    atomicMin(&best, mine);
+    if (take) pairs[atomicAdd(&n_pairs, 1u)] = k;  // order does not matter: the key decides
   }
+  __syncthreads();
+  const uint32_t np = n_pairs, nc = n_cuts;
+  unsigned long long mine = ~0ull;
+  for (uint32_t combo = t; combo < np * nc; combo += blockDim.x) {
+    const uint32_t k = pairs[combo / nc], A = cuts[combo % nc];
+    uint32_t cost = 0;
+    for (int i = 0; i < 16; ++i) cost += chroma_cost(chroma_desc_cut(sf[i], sd[i], fz[i], k, A));
+    const unsigned long long key = ((unsigned long long)cost << 17) | ((unsigned long long)k << 9) | A;
+    if (key < mine) mine = key;
+  }
+  if (mine != ~0ull) atomicMin(&best, mine);
   __syncthreads();
   const uint32_t bk = (uint32_t)(best >> 9) & 255u, bA = (uint32_t)best & 511u;
   if (!PALETTE) {
-    if (k == 0) {
+    if (t == 0) {
       ct->best[b] = best;
       atomicAdd(&ct->pair_hist[bk], 1u);
     }
     return;
   }
-  if (k < 16) ct->runs[c0 + k] = (uint16_t)chroma_desc_cut(sf[k], sd[k], fz[k], bk, bA);
-  if (k == 0) {
+  if (t < 16) ct->runs[c0 + t] = (uint16_t)chroma_desc_cut(sf[t], sd[t], fz[t], bk, bA);
+  if (t == 0) {
     ct->blocks[b] = (uint16_t)(ct->palette_of[bk] | (bA << 8));
     atomicAdd(&ct->flagged_cost, best >> 17);
   }
@@ -690,7 +723,8 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
           while (qn > 0) drain(qn < 64 ? qn : 64);
         if (total <= kHotQueueCap) {
           // entry index = the entries before this slot + the lane's rank (mbcnt
-          // accumulates the scalar count)
+          // accumulates the scalar count; measured faster than a v_lshl_add on
+          // an SGPR base, which waits for the SALU chain)
           uint32_t at = (uint32_t)qn;
 #pragma unroll
           for (int i = 0; i < CW; ++i) {
@@ -996,7 +1030,7 @@ int launch_nr(const KernelArgs& a, const ChromaGeom& g, const ChromaTables* ct, 
 }  // namespace
 
 int build_chroma_tables(const RangeTables* t, ChromaTables* ct, hipStream_t s) {
-  hipLaunchKernelGGL(chroma_summary_kernel, dim3(256), dim3(256), 0, s, t, ct);
+  hipLaunchKernelGGL(chroma_summary_kernel, dim3(1024), dim3(256), 0, s, t, ct);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(ct->pair_hist, 0, sizeof(ct->pair_hist), s);
