@@ -261,6 +261,7 @@ struct TrikCvHandle {
   uint32_t* d_maps = nullptr;
   size_t d_maps_cap = 0;
   int maps_key[6] = {-1, -1, -1, -1, -1, -1};
+  int32_t maps_rows2 = -1;  // first source row when the maps are the 2:1 ones, else -1
   std::vector<uint32_t> h_maps;
   StreamUses maps_users;
 
@@ -564,6 +565,13 @@ int32_t ensure_maps(TrikCvHandle* h, int w, int hgt, int ow, int oh, hipStream_t
   HIP_TRY(hipStreamSynchronize(s));  // h_maps is pageable and reused
   h->maps_key[0] = w; h->maps_key[1] = hgt; h->maps_key[2] = ow; h->maps_key[3] = oh;
   h->maps_key[4] = col_lo; h->maps_key[5] = col_hi;
+  // the 2:1 maps (the defaults' 640x480 -> 320x240): preview_rows2_kernel
+  const uint32_t* last_row = h->h_maps.data() + w + hgt;
+  const uint32_t* last_col = last_row + oh;
+  bool rows2 = oh > 0 && ow > 0 && (int32_t)last_row[0] >= 0;
+  for (int r = 0; rows2 && r < oh; ++r) rows2 = (int32_t)last_row[r] == (int32_t)last_row[0] + 2 * r;
+  for (int c = 0; rows2 && c < ow; ++c) rows2 = (int32_t)last_col[c] == 2 * c + 1;
+  h->maps_rows2 = rows2 ? (int32_t)last_row[0] : -1;
   return 0;
 }
 
@@ -587,6 +595,7 @@ PreviewArgs preview_args(const TrikCvHandle* h, const TrikHsvFrameBatch& b,
   a.hi2ho = a.wi2wo + b.width;
   a.last_row = reinterpret_cast<const int32_t*>(a.hi2ho + b.height);
   a.last_col = a.last_row + oh;
+  a.rows2_first = h->maps_rows2;
   return a;
 }
 

@@ -150,6 +150,9 @@ struct PreviewArgs {
   // ov7670 multi-blob preview: when set, a pixel is "detected" iff its 4x4
   // metapixel is set ([n][H/4][W/4], OSEQ:411-413) instead of by `range`
   const uint8_t* meta = nullptr;
+  // >= 0 when the maps are the 2:1 ones: last_row[r] = rows2_first + 2 r and
+  // last_col[c] = 2 c + 1 for every output row and column (preview_rows2_kernel)
+  int32_t rows2_first = -1;
 };
 
 // Auto HSV range of N frames (trik_hsv_operator.hip); out[f][6] = detectHue,

@@ -54,6 +54,9 @@ __constant__ Luts c_luts = make_luts();
 #ifndef TRIK_PREVIEW_MAP_LDS
 #define TRIK_PREVIEW_MAP_LDS 1
 #endif
+#ifndef TRIK_PREVIEW_ROWS2
+#define TRIK_PREVIEW_ROWS2 1  // the 2:1 row kernel where it applies
+#endif
 #ifndef TRIK_PREVIEW_Q
 #define TRIK_PREVIEW_Q 2
 #endif
@@ -174,6 +177,85 @@ void preview_gather_kernel(PreviewArgs a, PreviewGeom g) {
         *reinterpret_cast<uint32_t*>(row + b0) = out[u];
       } else {
         for (int k = 0; k < 4 && b0 + k < a.out_ll; ++k) row[b0 + k] = (uint8_t)(out[u] >> (8 * k));
+      }
+    }
+  }
+}
+
+// The same preview when the scale maps are the 2:1 ones (output row r' is
+// written last by source row r0 + 2 r', output column c' by source column
+// 2 c' + 1 -- the reference's defaults, 640x480 -> 320x240) for packed YUYV:
+// output pixel c' is the odd pixel of source word c', so a lane reads 4
+// consecutive words (16 bytes, one load; a wave reads 1 KiB of one row) and
+// writes 4 output pixels (8 bytes).  No maps, no gather.  kQ units per lane,
+// 64 apart, loads issued together.
+struct PreviewRowsGeom {
+  FastDiv per_frame;  // out_h * groups per row
+  FastDiv per_row;    // out_w / 4 groups per row
+  uint32_t total;
+};
+#ifndef TRIK_PREVIEW_ROWS_Q
+#define TRIK_PREVIEW_ROWS_Q 2
+#endif
+constexpr int kRowsQ = TRIK_PREVIEW_ROWS_Q;
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8)))
+void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
+  using namespace stripe_px;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  if (!a.meta) {
+    const u32x4* src = reinterpret_cast<const u32x4*>(a.tables);
+    typedef __attribute__((address_space(3))) u32x4* lds_u128_wptr;
+    lds_u128_wptr dst = (lds_u128_wptr)(uintptr_t)0;
+    for (int i = threadIdx.x; i < (int)(sizeof(StripeTables) / 16); i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+  }
+  const int t = threadIdx.x;
+  const uint32_t hue_lane = (uint32_t)offsetof(StripeTables, hue) + ((t % kHueCopies) << 2);
+  const uint32_t m43_lane = (uint32_t)offsetof(StripeTables, m43) + ((t % kM43Copies) << 2);
+  const uint32_t gpr = g.per_row.d, lane = t & 63u, wave_step = (gridDim.x * blockDim.x) >> 6;
+  const uint32_t n_chunks = (g.total + 64u * kRowsQ - 1) / (64u * kRowsQ);
+  for (uint32_t ch = (blockIdx.x * blockDim.x + t) >> 6; ch < n_chunks; ch += wave_step) {
+    uint32_t ff[kRowsQ], rr[kRowsQ], qq[kRowsQ];
+    bool ok[kRowsQ];
+    u32x4 w[kRowsQ];
+#pragma unroll
+    for (int u = 0; u < kRowsQ; ++u) {
+      const uint32_t i0 = ch * 64u * kRowsQ + 64u * u + lane;
+      ok[u] = i0 < g.total;
+      const uint32_t i = ok[u] ? i0 : 0u;  // past the end: re-read unit 0, not stored
+      ff[u] = fdiv(i, g.per_frame);
+      const uint32_t rem = i - ff[u] * g.per_frame.d;
+      rr[u] = fdiv(rem, g.per_row);
+      qq[u] = rem - rr[u] * gpr;
+      const int64_t sr = (int64_t)a.rows2_first + 2 * (int64_t)rr[u];
+      w[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
+          a.frames + (int64_t)ff[u] * a.frame_stride + sr * a.line_length + 16 * (int64_t)qq[u]));
+    }
+#pragma unroll
+    for (int u = 0; u < kRowsQ; ++u) {
+      const uint32_t ws[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+      uint32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const Phase1 p = phase1<1>(ws[k], ws[k] ^ 0xFF00FF00u, m43_lane);  // the odd pixel, Y1
+        uint32_t det;
+        if (a.meta) {
+          const int64_t sr = (int64_t)a.rows2_first + 2 * (int64_t)rr[u];
+          const int64_t sc = 2 * (4 * (int64_t)qq[u] + k) + 1;
+          det = a.meta[((int64_t)ff[u] * (a.height >> 2) + (sr >> 2)) * (a.width >> 2) + (sc >> 2)];
+        } else {
+          const uint32_t m = lds_u32(p.m43_addr), sv = lds_u8(p.sv_addr);
+          det = combine(lds_u32(phase2_addr(m, p, hue_lane)), sv) & 1u;
+        }
+        const uint32_t rgb = det ? 0x00ffffu : p.rgb888;
+        v[k] = ((rgb >> 19) & 0x001fu) | ((rgb >> 5) & 0x07e0u) | ((rgb << 8) & 0xf800u);
+      }
+      if (ok[u]) {
+        uint2 o;
+        o.x = v[0] | (v[1] << 16);
+        o.y = v[2] | (v[3] << 16);
+        *reinterpret_cast<uint2*>(a.previews + (int64_t)ff[u] * a.preview_stride + (int64_t)rr[u] * a.out_ll +
+                                  8 * (int64_t)qq[u]) = o;
       }
     }
   }
@@ -375,7 +457,37 @@ __global__ __launch_bounds__(kBlock) void auto_range_kernel(AutoRangeArgs a) {
 
 }  // namespace
 
+// The 2:1 row kernel when the maps, layout and alignment allow (see
+// preview_rows2_kernel); hipErrorNotSupported otherwise.
+static int launch_rows2(const PreviewArgs& a, hipStream_t s) {
+  if (a.rows2_first < 0 || a.layout != TRIK_HSV_LAYOUT_YUYV || a.out_w % 4 || a.out_ll != 2 * a.out_w ||
+      (!a.meta && !a.tables))
+    return hipErrorNotSupported;
+  const auto al = [](int64_t v, int64_t m) { return v % m == 0; };
+  if (!al((int64_t)reinterpret_cast<uintptr_t>(a.frames), 16) || !al(a.line_length, 16) ||
+      (a.n_frames > 1 && !al(a.frame_stride, 16)) || !al((int64_t)reinterpret_cast<uintptr_t>(a.previews), 8) ||
+      (a.n_frames > 1 && !al(a.preview_stride, 8)))
+    return hipErrorNotSupported;
+  const int64_t gpr = a.out_w / 4, total = (int64_t)a.n_frames * a.out_h * gpr;
+  if (total >= (1ll << 31)) return hipErrorNotSupported;
+  if (total == 0) return hipSuccess;
+  hipError_t e = set_dynamic_lds(reinterpret_cast<const void*>(preview_rows2_kernel), 80 * 1024);
+  if (e != hipSuccess) return e;
+  PreviewRowsGeom g;
+  g.per_frame = make_div((uint32_t)(a.out_h * gpr));
+  g.per_row = make_div((uint32_t)gpr);
+  g.total = (uint32_t)total;
+  const int64_t blocks = (total + 1024LL * kRowsQ - 1) / (1024LL * kRowsQ), slots = 2LL * device_cus();
+  hipLaunchKernelGGL(preview_rows2_kernel, dim3((unsigned)(blocks < slots ? blocks : slots)), dim3(1024),
+                     a.meta ? 0 : sizeof(StripeTables), s, a, g);
+  return hipGetLastError();
+}
+
 static int launch_gather(const PreviewArgs& a, hipStream_t s) {
+  if (TRIK_PREVIEW_ROWS2) {
+    const int e = launch_rows2(a, s);
+    if (e != hipErrorNotSupported) return e;
+  }
   const int64_t qpr = (a.out_ll + 3) / 4, total = (int64_t)a.n_frames * a.out_h * qpr;
   if (total >= (1ll << 31) || (!a.meta && !a.tables)) return hipErrorInvalidValue;
   if (total == 0) return hipSuccess;
