@@ -293,6 +293,20 @@ int32_t TRIK_VIDTRANSCODE_CV_create(const TRIK_VIDTRANSCODE_CV_Params* params,
 int32_t TRIK_VIDTRANSCODE_CV_create_line(const TRIK_VIDTRANSCODE_CV_Params* params,
                                          TRIK_VIDTRANSCODE_CV_Handle* out_handle);
 
+/* The quartet for the webcam line sensor's codec (trik/webcam/line_sensor,
+ * LineDetector<YUV422, RGB565X> of include/internal/
+ * cv_line_detector_seqpass.hpp -- LSEQW).  params == NULL takes the webcam
+ * glue's defaults (YUV422 = packed YUYV in, RGB565X out; default dynamic
+ * output 240 wide x 320 high).  process() runs LineDetector::run (LSEQW:
+ * 330-420): the range (H 0..359, S 0..100, V detectValFrom..detectValTo)
+ * over every pixel; when more than 10 pixels match, targetX = ((x - W/2) *
+ * 200) / W of the mean column, targetY = 0, targetSize = N * 100 / (W * H);
+ * the preview is every pixel (matches white) with magenta lines at columns
+ * W/2 +- 40 and +- 80 and a red 3-column line at the mean column.
+ * autoDetectHsv is ignored (its detector is seeded by srand(time(NULL))). */
+int32_t TRIK_VIDTRANSCODE_CV_create_webcam_line(const TRIK_VIDTRANSCODE_CV_Params* params,
+                                                TRIK_VIDTRANSCODE_CV_Handle* out_handle);
+
 /* The quartet for the ov7670 object sensor's codec (trik/ov7670/object_sensor:
  * BallDetector<YUV422P, RGB565X> of include/internal/
  * cv_ball_detector_seqpass.hpp:516-602 -- OSEQ -- with its BitmapBuilder and
@@ -385,13 +399,15 @@ typedef struct TRIK_IVIDTRANSCODE_Fxns {
 
 /* The webcam object sensor's tables (WFXNS:36-66); IALG is the same table
  * as FXNS.ialg (the reference aliases the two symbols on TI toolchains and
- * duplicates them elsewhere, as here).  The other two codecs of this library
+ * duplicates them elsewhere, as here).  The other three codecs of this library
  * (one DSP server each in the reference, all named TRIK_VIDTRANSCODE_CV_FXNS
- * there): the ov7670 object sensor and the ov7670 line sensor. */
+ * there): the ov7670 object sensor, the ov7670 line sensor and the webcam
+ * line sensor. */
 extern TRIK_IVIDTRANSCODE_Fxns TRIK_VIDTRANSCODE_CV_FXNS;
 extern TRIK_IALG_Fxns TRIK_VIDTRANSCODE_CV_IALG;
 extern TRIK_IVIDTRANSCODE_Fxns TRIK_VIDTRANSCODE_CV_OV7670_FXNS;
 extern TRIK_IVIDTRANSCODE_Fxns TRIK_VIDTRANSCODE_CV_LINE_FXNS;
+extern TRIK_IVIDTRANSCODE_Fxns TRIK_VIDTRANSCODE_CV_WEBCAM_LINE_FXNS;
 
 /* The webcam object sensor's IALG functions (WFXNS:85-166), also reachable
  * through the tables.  alloc asks for one persistent external record (the

@@ -113,6 +113,9 @@ def lib():
                                            vp, C.c_int, C.c_int, C.c_int, vp, i64,
                                            C.POINTER(OutArgs), vp]
         L.trik_oracle_line_run.restype = C.c_int
+        L.trik_oracle_wline_run.argtypes = [vp, i64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                            C.c_int, C.c_int, C.c_int, vp, i64, C.POINTER(OutArgs), vp]
+        L.trik_oracle_wline_run.restype = C.c_int
         L.trik_oracle_blob_range.argtypes = [C.POINTER(BlobArgs), C.POINTER(BlobState)]
         L.trik_oracle_blob_range.restype = None
         L.trik_oracle_blob_run.argtypes = [vp, i64, C.c_int, C.c_int, C.c_int, C.POINTER(BlobArgs),
@@ -263,6 +266,23 @@ def line_run(frame_u8: np.ndarray, width, height, line_length, val_from, val_to,
     return rc, d, (out[:oh * oll] if out is not None else None), sums, tuple(int(v) for v in b)
 
 
+def wline_run(frame_u8: np.ndarray, width, height, line_length, val_from, val_to, out_width=240,
+              out_height=320, out_line_length=None, preview=True):
+    """LineDetector::setup + run (webcam line sensor) for one YUYV frame; the
+    default preview is that glue's 240 wide x 320 high.  Returns (rc, outargs
+    dict, preview or None, sums[3])."""
+    fr = np.ascontiguousarray(frame_u8, dtype=np.uint8)
+    oll = 2 * out_width if out_line_length is None else out_line_length
+    out = np.zeros(max(1, out_height * oll), np.uint8) if preview else None
+    sums = np.zeros(3, np.int64)
+    oa = OutArgs()
+    rc = lib().trik_oracle_wline_run(_ptr(fr), fr.size, width, height, line_length, val_from, val_to,
+                                     out_width, out_height, oll, _ptr(out) if out is not None else None,
+                                     out.size if out is not None else 0, C.byref(oa), _ptr(sums))
+    d = {k: getattr(oa, k) for k, _ in OutArgs._fields_}
+    return rc, d, (out[:out_height * oll] if out is not None else None), sums
+
+
 def line_scene(width, height, line_length, seed, x0=None, slope=0.25, line_w=24) -> np.ndarray:
     """A test ov7670 (YUV422P) frame for the line sensor: a bright textured
     floor with a dark slanted line, random bytes in the row padding (inputs for
@@ -279,6 +299,24 @@ def line_scene(width, height, line_length, seed, x0=None, slope=0.25, line_w=24)
         lo, hi = max(0, a), min(width, a + line_w)
         if lo < hi:
             y[r, lo:hi] = rng.integers(10, 50, hi - lo)
+    return fr
+
+
+def wline_scene(width, height, line_length, seed, x0=None, slope=0.25, line_w=24) -> np.ndarray:
+    """A test packed-YUYV frame for the webcam line sensor: a bright textured
+    floor with a dark slanted line, random bytes in the row padding (inputs for
+    the parity tests; not a reference fixture)."""
+    rng = np.random.default_rng(seed)
+    fr = rng.integers(0, 256, height * line_length, dtype=np.uint8)
+    img = fr.reshape(height, line_length)
+    img[:, 0:2 * width:2] = rng.integers(150, 230, (height, width))   # Y
+    img[:, 1:2 * width:2] = rng.integers(108, 148, (height, width))   # U / V
+    x0 = width // 2 if x0 is None else x0
+    for r in range(height):
+        a = int(x0 + slope * (r - height / 2))
+        lo, hi = max(0, a), min(width, a + line_w)
+        if lo < hi:
+            img[r, 2 * lo:2 * hi:2] = rng.integers(10, 50, hi - lo)
     return fr
 
 

@@ -790,6 +790,88 @@ int trik_oracle_line_run(const uint8_t* frame, int64_t frame_size, int width, in
 }
 
 /* ------------------------------------------------------------------------ */
+/* webcam line sensor (LSEQW = trik/webcam/line_sensor/include/internal/     */
+/* cv_line_detector_seqpass.hpp).                                            */
+/* ------------------------------------------------------------------------ */
+
+int trik_oracle_wline_run(const uint8_t* frame, int64_t frame_size, int width, int height,
+                          int line_length, int val_from, int val_to, int out_width, int out_height,
+                          int out_line_length, uint8_t* out, int64_t out_size, trik_oracle_outargs* oa,
+                          int64_t sums[3]) {
+  memset(oa, 0, sizeof *oa);
+  if (width < 0 || height < 0 || width % 32 != 0 || height % 4 != 0) return -1; /* LSEQW:297-301 */
+  if ((int64_t)height * line_length > frame_size) return -1;                    /* LSEQW:333 */
+  if (out && (int64_t)out_height * out_line_length > out_size) return -1;       /* LSEQW:335 */
+
+  /* LSEQW:304-305: the smaller of the two output/input ratios, in double */
+  const double rw = (double)out_width / width, rh = (double)out_height / height;
+  const double shift = rh < rw ? rh : rw;
+  uint32_t* col_map = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(width > 0 ? width : 1));
+  uint32_t* row_map = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(height > 0 ? height : 1));
+  if (!col_map || !row_map) {
+    free(col_map); free(row_map);
+    return -1;
+  }
+  for (int c = 0; c < width; ++c) col_map[c] = (uint32_t)(c * shift);
+  for (int r = 0; r < height; ++r) row_map[r] = (uint32_t)(r * shift);
+
+  /* LSEQW:345-364: H 0..255 and S 0..255 (unscaled constants), V scaled and
+   * clamped as the object sensor does; never the wrapped-hue form */
+  const trik_oracle_range vr = {0, 0, 0, 0, (uint8_t)val_from, (uint8_t)val_to};
+  uint32_t lo, hi, expect;
+  trik_oracle_pack_range(&vr, &lo, &hi, &expect);
+  lo &= 0x00FF0000u;
+  hi = (hi & 0x00FF0000u) | 0x0000FFFFu;
+
+  /* LSEQW:197-269 with m_imageScaleCoeff = 1: every row, first row 0 */
+  int32_t acc_x = 0, acc_y = 0;
+  uint32_t acc_n = 0;
+  for (int row = 0; row < height; ++row) {
+    uint32_t n_row = 0, x_row = 0;
+    for (int q = 0; q < width / 2; ++q) {
+      uint32_t rgb[2];
+      trik_oracle_pair_rgb_c64x(pair_word(frame, height, line_length, TRIK_ORACLE_LAYOUT_YUYV, row, q), rgb);
+      for (int k = 0; k < 2; ++k) {
+        const int col = 2 * q + k;
+        const int hit = trik_oracle_detect(trik_oracle_hsv_c64x(rgb[k]), lo, hi, 0);
+        n_row += (uint32_t)hit;
+        x_row += hit ? (uint32_t)col : 0u;
+        if (out)
+          write_px(out + (int64_t)row_map[row] * out_line_length + (int64_t)col_map[col] * 2,
+                   hit ? 0x00ffffu : rgb[k]);
+      }
+    }
+    acc_x += (int32_t)x_row;
+    acc_y += (int32_t)((uint32_t)row * n_row);
+    acc_n += n_row;
+  }
+
+  const run_ctx ctx = {width, height, out_line_length, col_map, row_map, out};
+  const int mid = width / 2;
+  if (out && width > 0 && height > 0) { /* drawRgbThinLine x4 from row 0 (LSEQW:396-399) */
+    const int32_t at[4] = {mid - 40, mid + 40, mid - 80, mid + 80};
+    for (int k = 0; k < 4; ++k)
+      for (int r = 0; r < height; ++r) draw_bound(&ctx, at[k], r, 0xff00ff);
+  }
+  if (acc_n > 10) { /* LSEQW:405-417 */
+    const int32_t tx = (int32_t)((uint32_t)acc_x / acc_n);
+    if (out)
+      for (int r = 0; r < height; ++r) /* drawRgbTargetCenterLine */
+        for (int c = tx - 1; c <= tx + 1; ++c) draw_bound(&ctx, c, r, 0xff0000);
+    oa->target_x = (int8_t)(((tx - width / 2) * 200) / width);
+    oa->target_size = (uint8_t)((acc_n * 100u) / (uint32_t)(width * height));
+  }
+  if (sums) {
+    sums[0] = (int64_t)acc_n;
+    sums[1] = (int64_t)acc_x;
+    sums[2] = (int64_t)acc_y;
+  }
+  free(col_map);
+  free(row_map);
+  return 0;
+}
+
+/* ------------------------------------------------------------------------ */
 /* ov7670 object sensor: metapixel bitmap + clusterer (OSEQ:516-602).        */
 /* ------------------------------------------------------------------------ */
 

@@ -176,6 +176,21 @@ int      trik_oracle_line_run(const uint8_t* frame, int64_t frame_size, int widt
                               int out_width, int out_height, int out_line_length, uint8_t* out,
                               int64_t out_size, trik_oracle_outargs* oa, int64_t sums[3]);
 
+/* The webcam line sensor, LineDetector<YUV422, RGB565X>::setup + run
+ * (trik/webcam/line_sensor/include/internal/cv_line_detector_seqpass.hpp:
+ * 290-420; LSEQW): packed YUYV, the object sensor's per-pixel HSV, detection
+ * by V only (H and S bounds 0..255), every pixel of every row
+ * (m_imageScaleCoeff = 1); the preview written for every pixel through the
+ * object sensor's maps, four thin magenta lines at columns W/2 +- 40 and
+ * W/2 +- 80, and, when N > 10, the 3-column red target line; OutArgs
+ * targetX as the object sensor, targetY 0, targetSize = N * 100 / (W * H),
+ * all 0 unless N > 10.  autoDetectHsv is not restated (simulated annealing
+ * seeded by srand(time(NULL))).  sums (optional) receives {N, sumX, sumY}. */
+int      trik_oracle_wline_run(const uint8_t* frame, int64_t frame_size, int width, int height,
+                               int line_length, int val_from, int val_to, int out_width,
+                               int out_height, int out_line_length, uint8_t* out, int64_t out_size,
+                               trik_oracle_outargs* oa, int64_t sums[3]);
+
 /* ---- ov7670 object sensor: metapixel bitmap + clusterer -> 8 targets ------
  * BLOB = BallDetector<YUV422P, RGB565X> of trik/ov7670/object_sensor/include/
  * internal/cv_ball_detector_seqpass.hpp:516-602 (OSEQ), with BitmapBuilder

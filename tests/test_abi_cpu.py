@@ -34,6 +34,7 @@ def test_header_declares_the_quartet_and_batch_api():
               "trik_hsv_process_batch", "trik_hsv_batch_sums", "trik_hsv_batch_targets",
               "trik_hsv_batch_masks", "trik_hsv_synth", "trik_hsv_version", "trik_hsv_last_error",
               "TRIK_VIDTRANSCODE_CV_create_line", "TRIK_VIDTRANSCODE_CV_create_ov7670",
+              "TRIK_VIDTRANSCODE_CV_create_webcam_line",
               "trik_hsv_line_batch", "trik_hsv_line_preview", "trik_hsv_blob_batch", "trik_hsv_blob_preview",
               "trik_hsv_batch_preview", "trik_hsv_batch_auto_range"):
         assert n in names
@@ -98,9 +99,9 @@ XDAIS_PROG = r"""
 #include "trik_hsv.h"
 /* a Codec-Engine-style caller that binds only the function tables */
 int main(void) {
-  const TRIK_IVIDTRANSCODE_Fxns* tabs[3] = {&TRIK_VIDTRANSCODE_CV_FXNS, &TRIK_VIDTRANSCODE_CV_OV7670_FXNS,
-                                            &TRIK_VIDTRANSCODE_CV_LINE_FXNS};
-  for (int i = 0; i < 3; ++i) {
+  const TRIK_IVIDTRANSCODE_Fxns* tabs[4] = {&TRIK_VIDTRANSCODE_CV_FXNS, &TRIK_VIDTRANSCODE_CV_OV7670_FXNS,
+                                            &TRIK_VIDTRANSCODE_CV_LINE_FXNS, &TRIK_VIDTRANSCODE_CV_WEBCAM_LINE_FXNS};
+  for (int i = 0; i < 4; ++i) {
     const TRIK_IVIDTRANSCODE_Fxns* f = tabs[i];
     TRIK_IALG_MemRec m[16];
     TRIK_IALG_Fxns* parent = NULL;
@@ -128,4 +129,4 @@ def test_xdais_tables_link_from_c_and_alloc_without_gpu():
                         f"-L{lib_dir}", "-ltrik_hsv", f"-Wl,-rpath,{lib_dir}", "-o", exe], check=True)
         r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
-    assert len(r.stdout.split("\n")) >= 3
+    assert len(r.stdout.split("\n")) >= 4

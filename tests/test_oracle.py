@@ -179,3 +179,41 @@ def test_cpu_baseline_equals_oracle(oracle_mod, layout, kind, n_ranges):
     want, _ = o.batch(frames, stride, 6, w, h, ll, layout, ranges)
     got = o.cpu_batch(frames, stride, 6, w, h, ll, layout, ranges, n_threads=3)
     assert np.array_equal(got, want)
+
+
+# --- the webcam line sensor restatement (trik_oracle_wline_run, LSEQW) ---
+@pytest.mark.parametrize("vf,vt", [(0, 30), (50, 100), (80, 20), (0, 100)])
+def test_wline_sums_are_the_object_sensor_sums_of_its_range(oracle_mod, vf, vt):
+    """LSEQW's detection is the object sensor's with H 0..359, S 0..100 (both
+    0..255 after scaling, LSEQW:345-364): its {N, sumX, sumY} equal
+    trik_oracle_frame's for that range; the OutArgs follow LSEQW:405-417."""
+    o = oracle_mod
+    w, h, ll = 320, 240, 672
+    fr = o.wline_scene(w, h, ll, 5, slope=-0.3)
+    rc, oa, pv, sums = o.wline_run(fr, w, h, ll, vf, vt, out_width=160, out_height=120)
+    assert rc == 0
+    want, _ = o.frame(fr, w, h, ll, o.LAYOUT_YUYV, [(0, 359, 0, 100, vf, vt)])
+    assert sums.tolist() == want[0].tolist()
+    n, sx = int(sums[0]), int(sums[1])
+    if n > 10:
+        tx = (sx & 0xFFFFFFFF) // n
+        assert oa["target_x"] == int(np.int8(int(((tx - w // 2) * 200) / w)))
+        assert oa["target_size"] == (n * 100) // (w * h) % 256
+    else:
+        assert (oa["target_x"], oa["target_size"]) == (0, 0)
+    assert oa["target_y"] == 0
+    # thin lines (magenta, 0xff00ff -> RGB565X 0x1ff8 little-endian) over every output row
+    img = pv.reshape(120, 320)
+    for c in (w // 2 - 80, w // 2 - 40, w // 2 + 40, w // 2 + 80):
+        oc = int(c * 0.5)
+        if n <= 10 or abs(c - (sx & 0xFFFFFFFF) // n) > 3:
+            assert (img[:, 2 * oc] == 0x1f).all() and (img[:, 2 * oc + 1] == 0xf8).all(), c
+
+
+def test_wline_rejects_and_empty(oracle_mod):
+    o = oracle_mod
+    assert o.wline_run(np.zeros(64 * 8, np.uint8), 48, 4, 96, 0, 30)[0] != 0      # W % 32
+    assert o.wline_run(np.zeros(64 * 8, np.uint8), 32, 6, 64, 0, 30)[0] != 0      # H % 4
+    assert o.wline_run(np.zeros(64 * 8, np.uint8), 32, 16, 64, 0, 30)[0] != 0     # short input
+    rc, oa, pv, sums = o.wline_run(np.zeros(16, np.uint8), 0, 0, 0, 0, 30, out_width=0, out_height=0)
+    assert rc == 0 and sums.tolist() == [0, 0, 0] and not pv.any()

@@ -64,7 +64,10 @@ const TRIK_VIDTRANSCODE_CV_Params k_default_params = {{
 // LSEQ = trik/ov7670/line_sensor/include/internal/cv_line_detector_seqpass.hpp;
 // its glue trik/ov7670/line_sensor/src/vidtranscode_cv.cpp is WGLUE with
 // YUV422P input and a 240x320 default output).
-enum Algo { kAlgoBall = 0, kAlgoLine = 1, kAlgoBlob = 2 };
+// kAlgoWLine: the webcam line sensor (LineDetector<YUV422, RGB565X> of
+// trik/webcam/line_sensor/include/internal/cv_line_detector_seqpass.hpp --
+// LSEQW -- with the webcam glue, a 240x320 default output as the line glues).
+enum Algo { kAlgoBall = 0, kAlgoLine = 1, kAlgoBlob = 2, kAlgoWLine = 3 };
 
 // ov7670 object sensor glue: the webcam glue with formatInput = YUV422P
 // (trik/ov7670/object_sensor/src/vidtranscode_cv.cpp:80,157)
@@ -99,8 +102,9 @@ TRIK_VIDTRANSCODE_CV_DynamicParams default_dynamic_params(int algo) {  // WGLUE:
   d.base.readHeaderOnlyFlag = 0;
   d.base.keepInputResolutionFlag[0] = 0;
   d.base.keepInputResolutionFlag[1] = 1;
-  d.base.outputHeight[0] = algo == kAlgoLine ? 320 : 240;  // line glue :214,218 swaps them
-  d.base.outputWidth[0] = algo == kAlgoLine ? 240 : 320;
+  const bool line = algo == kAlgoLine || algo == kAlgoWLine;
+  d.base.outputHeight[0] = line ? 320 : 240;  // the line glues (:214,218) swap them
+  d.base.outputWidth[0] = line ? 240 : 320;
   d.base.keepInputFrameRateFlag[0] = d.base.keepInputFrameRateFlag[1] = 1;
   d.base.inputFrameRate = -1;
   d.base.outputFrameRate[0] = d.base.outputFrameRate[1] = -1;
@@ -351,9 +355,11 @@ int32_t setup_image_desc(TrikCvHandle* h) {
   if (h->algo == kAlgoBlob &&
       (in_w > 8192 || blob_max_labels(in_w / 4, in_h / 4) > 30000))  // uint16 labels, LDS
     return fail(TRIK_IALG_EFAIL, "CV algorithm setup failed: frame too large for the multi-blob sensor");
-  if (h->algo == kAlgoBall && in_fmt == TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_YUV422 && out_ok)
+  if ((h->algo == kAlgoBall || h->algo == kAlgoWLine) && in_fmt == TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_YUV422 &&
+      out_ok)
     layout = TRIK_HSV_LAYOUT_YUYV;
-  else if (in_fmt == TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_YUV422P && out_ok)  // line: YUV422P only
+  else if (h->algo != kAlgoWLine && in_fmt == TRIK_VIDTRANSCODE_CV_VIDEO_FORMAT_YUV422P &&
+           out_ok)  // ov7670 line: YUV422P only; webcam line: YUV422 only
     layout = TRIK_HSV_LAYOUT_OV7670;
   else
     return fail(TRIK_IALG_EFAIL, "cannot create CV algorithm for this format pair");
@@ -778,11 +784,15 @@ AutoRangeArgs auto_range_args(const TrikHsvFrameBatch& b, uint16_t* out) {
 // Layer 1: XDAIS-shaped quartet
 // ---------------------------------------------------------------------------
 extern "C" TRIK_IVIDTRANSCODE_Fxns TRIK_VIDTRANSCODE_CV_FXNS, TRIK_VIDTRANSCODE_CV_OV7670_FXNS,
-    TRIK_VIDTRANSCODE_CV_LINE_FXNS;
+    TRIK_VIDTRANSCODE_CV_LINE_FXNS, TRIK_VIDTRANSCODE_CV_WEBCAM_LINE_FXNS;
 
 static const TRIK_IALG_Fxns* table_of(int algo) {
-  return algo == kAlgoLine ? &TRIK_VIDTRANSCODE_CV_LINE_FXNS.ialg
-                           : (algo == kAlgoBlob ? &TRIK_VIDTRANSCODE_CV_OV7670_FXNS.ialg : &TRIK_VIDTRANSCODE_CV_FXNS.ialg);
+  switch (algo) {
+    case kAlgoLine: return &TRIK_VIDTRANSCODE_CV_LINE_FXNS.ialg;
+    case kAlgoBlob: return &TRIK_VIDTRANSCODE_CV_OV7670_FXNS.ialg;
+    case kAlgoWLine: return &TRIK_VIDTRANSCODE_CV_WEBCAM_LINE_FXNS.ialg;
+    default: return &TRIK_VIDTRANSCODE_CV_FXNS.ialg;
+  }
 }
 
 // trikCvHandleInit + SetupParams + SetupDynamicParams (WFXNS:146-166) on a
@@ -796,6 +806,7 @@ static int32_t init_handle(TrikCvHandle* h, int algo, const TRIK_VIDTRANSCODE_CV
   h->params = params ? *params
                      : (algo == kAlgoLine ? k_default_params_line
                                           : (algo == kAlgoBlob ? k_default_params_blob : k_default_params));  // WGLUE:188-191
+  // (the webcam line sensor's glue has the webcam object sensor's Params)
   const int32_t rc = setup_dynamic(h, nullptr);      // WFXNS:158-163
   if (rc != TRIK_IALG_EOK) {
     release(h);
@@ -824,6 +835,11 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_create(const TRIK_VIDTRANSCODE_CV_Params
 extern "C" int32_t TRIK_VIDTRANSCODE_CV_create_line(const TRIK_VIDTRANSCODE_CV_Params* params,
                                                     TRIK_VIDTRANSCODE_CV_Handle* out_handle) {
   return create_handle(kAlgoLine, params, out_handle);
+}
+
+extern "C" int32_t TRIK_VIDTRANSCODE_CV_create_webcam_line(const TRIK_VIDTRANSCODE_CV_Params* params,
+                                                           TRIK_VIDTRANSCODE_CV_Handle* out_handle) {
+  return create_handle(kAlgoWLine, params, out_handle);
 }
 
 extern "C" int32_t TRIK_VIDTRANSCODE_CV_create_ov7670(const TRIK_VIDTRANSCODE_CV_Params* params,
@@ -923,6 +939,9 @@ static int32_t ialg_init_blob(TRIK_IALG_Handle a, const TRIK_IALG_MemRec* m, TRI
 static int32_t ialg_init_line(TRIK_IALG_Handle a, const TRIK_IALG_MemRec* m, TRIK_IALG_Handle, const TRIK_IALG_Params* p) {
   return ialg_init(kAlgoLine, a, m, p);
 }
+static int32_t ialg_init_wline(TRIK_IALG_Handle a, const TRIK_IALG_MemRec* m, TRIK_IALG_Handle, const TRIK_IALG_Params* p) {
+  return ialg_init(kAlgoWLine, a, m, p);
+}
 
 // algFree: the object is destroyed; its record is returned for the framework
 static int32_t ialg_free(TRIK_IALG_Handle alg, TRIK_IALG_MemRec mem_tab[]) {
@@ -962,6 +981,8 @@ TRIK_IVIDTRANSCODE_Fxns TRIK_VIDTRANSCODE_CV_OV7670_FXNS = {
     TRIK_IALGFXNS(TRIK_VIDTRANSCODE_CV_OV7670_FXNS, ialg_init_blob), xdais_process, xdais_control};
 TRIK_IVIDTRANSCODE_Fxns TRIK_VIDTRANSCODE_CV_LINE_FXNS = {TRIK_IALGFXNS(TRIK_VIDTRANSCODE_CV_LINE_FXNS, ialg_init_line),
                                                           xdais_process, xdais_control};
+TRIK_IVIDTRANSCODE_Fxns TRIK_VIDTRANSCODE_CV_WEBCAM_LINE_FXNS = {
+    TRIK_IALGFXNS(TRIK_VIDTRANSCODE_CV_WEBCAM_LINE_FXNS, ialg_init_wline), xdais_process, xdais_control};
 }
 
 extern "C" int32_t TRIK_VIDTRANSCODE_CV_alloc(const TRIK_IALG_Params* params, TRIK_IALG_Fxns** parent_fxns,
@@ -1139,6 +1160,37 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
           // are left untouched.
           h->line_band[0] = h->in_h / 2;  // LSEQ:449-450, read by the next run
           h->line_band[1] = h->in_h / 2 + 80;
+          return 0;
+        }
+        if (h->algo == kAlgoWLine) {  // webcam LineDetector::run, LSEQW:330-420
+          // hue and saturation fixed to the full bytes, V from InArgs (LSEQW:345-351)
+          const TRIK_VIDTRANSCODE_CV_InArgsAlg wr = line_alg(in_args->alg.detectValFrom, in_args->alg.detectValTo);
+          int32_t r = run_sums(h, &b, &wr, 1, h->d_sums, nullptr, h->stream);
+          if (r) return r;
+          HIP_TRY(launch_wline_targets(1, h->in_w, h->in_h, h->d_sums, h->d_targets, h->stream));
+          if (out_ptr && out_size > 0) {  // every pixel (LSEQW:232-269), then the thin and target lines
+            const size_t pb = (size_t)out_size;
+            r = grow(h->d_preview, h->d_preview_cap, pb);
+            if (r) return r;
+            r = ensure_maps(h, h->in_w, h->in_h, h->out_w, h->out_h, h->stream);
+            if (r) return r;
+            PreviewArgs pa = preview_args(h, b, wr, h->out_w, h->out_h, h->out_ll, h->d_preview, (int64_t)pb);
+            TableSet* set = nullptr;
+            r = preview_tables(h, pa, wr, h->stream, &set);
+            if (r) return r;
+            HIP_TRY(launch_preview_body(pa, h->stream));
+            HIP_TRY(launch_wline_overlay(pa, h->d_sums, h->stream));
+            r = note_uses(h, set, true, h->stream);
+            if (r) return r;
+            HIP_TRY(hipMemcpyAsync(out_ptr, h->d_preview, pb, hipMemcpyDeviceToHost, h->stream));
+          }
+          TrikHsvTarget t;
+          HIP_TRY(hipMemcpyAsync(&t, h->d_targets, sizeof t, hipMemcpyDeviceToHost, h->stream));
+          HIP_TRY(hipStreamSynchronize(h->stream));
+          oa.targetX = t.x; oa.targetY = t.y; oa.targetSize = t.size;
+          // autoDetectHsv: this sensor's range detector is a simulated annealing
+          // seeded by srand(time(NULL)) (its cv_hsv_range_detector.hpp:200) --
+          // not reproducible; detect* are left untouched.
           return 0;
         }
         int32_t r = run_sums(h, &b, &in_args->alg, 1, h->d_sums, nullptr, h->stream);

@@ -211,6 +211,11 @@ int launch_line(const LineArgs& a, hipStream_t s);
 // preview body as launch_preview's first kernel, then the line sensor's overlay
 int launch_preview_body(const PreviewArgs& a, hipStream_t s);
 int launch_line_overlay(const PreviewArgs& a, const TrikHsvTargetSums* sums, hipStream_t s);
+// the webcam line sensor (trik/webcam/line_sensor): OutArgs from the sums of
+// the V-only range (targetY 0), and its overlay (thin lines, target line)
+int launch_wline_targets(int n_frames, int width, int height, const TrikHsvTargetSums* sums, TrikHsvTarget* targets,
+                         hipStream_t s);
+int launch_wline_overlay(const PreviewArgs& a, const TrikHsvTargetSums* sums, hipStream_t s);
 
 // ov7670 multi-blob sensor of N frames (trik_hsv_blob.hip).
 struct BlobArgs {

@@ -222,8 +222,10 @@ __global__ __launch_bounds__(kLineBlock) void line_sums_kernel(LineArgs a) {
   }
 }
 
+// cross = false: the webcam line sensor (LSEQW:401-417: targetY stays 0,
+// the sum_y slot holds the plain row sums)
 __global__ void line_targets_kernel(int n_frames, int width, int height, const TrikHsvTargetSums* sums,
-                                    TrikHsvTarget* targets) {
+                                    TrikHsvTarget* targets, int cross = 1) {
   const int f = blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= n_frames) return;
   const TrikHsvTargetSums s = sums[f];
@@ -232,13 +234,16 @@ __global__ void line_targets_kernel(int n_frames, int width, int height, const T
   if (n > 10) {  // LSEQ:462-474 (crossSize LSEQ:452, step 40)
     const int32_t cx = (int32_t)((uint32_t)(int32_t)s.sum_x / n);
     t.x = (int8_t)(((cx - width / 2) * 100 * 2) / width);
-    t.y = (int8_t)(int)((uint32_t)((uint32_t)s.sum_y * 100u) / (uint32_t)(width * 2 * 40));
+    t.y = cross ? (int8_t)(int)((uint32_t)((uint32_t)s.sum_y * 100u) / (uint32_t)(width * 2 * 40)) : (int8_t)0;
     t.size = (uint8_t)((uint32_t)(n * 100u) / (uint32_t)(height * width));
   }
   targets[f] = t;
 }
 
-__global__ __launch_bounds__(64) void line_overlay_kernel(PreviewArgs a, const TrikHsvTargetSums* sums) {
+// band = false: the webcam line sensor (LSEQW:396-399, 405-413): the four
+// thin lines and the target line, no band lines
+__global__ __launch_bounds__(64) void line_overlay_kernel(PreviewArgs a, const TrikHsvTargetSums* sums,
+                                                          int band = 1) {
   const int f = blockIdx.x, lane = threadIdx.x;
   uint8_t* out = a.previews + (int64_t)f * a.preview_stride;
   const int W = a.width, H = a.height, step = 40;
@@ -251,7 +256,8 @@ __global__ __launch_bounds__(64) void line_overlay_kernel(PreviewArgs a, const T
   const int32_t cols[4] = {hw - step, hw + step, hw - 2 * step, hw + 2 * step};
   for (int k = lane; k < 4 * H; k += 64) px(cols[k / H], k % H, 0xff00ff);  // drawRgbThinLine, rows 0..H-1
   __syncthreads();
-  for (int k = lane; k < 2 * W; k += 64) px(k % W, k < W ? hh : hh + 2 * step, 0xff0000);  // band lines
+  if (band)
+    for (int k = lane; k < 2 * W; k += 64) px(k % W, k < W ? hh : hh + 2 * step, 0xff0000);  // band lines
   const TrikHsvTargetSums s = sums[f];
   const uint32_t n = (uint32_t)s.points;
   if (n > 10) {  // drawRgbTargetCenterLine(targetX, 0), LSEQ:88-102
@@ -315,6 +321,20 @@ int launch_line(const LineArgs& a, hipStream_t s) {
   if (e != hipSuccess || !a.targets) return e;
   hipLaunchKernelGGL(line_targets_kernel, dim3((unsigned)((a.n_frames + 255) / 256)), dim3(256), 0, s,
                      a.n_frames, a.width, a.height, a.sums, a.targets);
+  return hipGetLastError();
+}
+
+int launch_wline_targets(int n_frames, int width, int height, const TrikHsvTargetSums* sums, TrikHsvTarget* targets,
+                         hipStream_t s) {
+  if (n_frames <= 0 || !targets) return hipSuccess;
+  hipLaunchKernelGGL(line_targets_kernel, dim3((unsigned)((n_frames + 255) / 256)), dim3(256), 0, s, n_frames, width,
+                     height, sums, targets, 0);
+  return hipGetLastError();
+}
+
+int launch_wline_overlay(const PreviewArgs& a, const TrikHsvTargetSums* sums, hipStream_t s) {
+  if (a.n_frames <= 0 || a.width <= 0 || a.height <= 0) return hipSuccess;
+  hipLaunchKernelGGL(line_overlay_kernel, dim3((unsigned)a.n_frames), dim3(64), 0, s, a, sums, 0);
   return hipGetLastError();
 }
 

@@ -521,6 +521,15 @@ class LineSensor(ObjectSensor):
             self.params = _default_params(1, fmt_in=FORMAT_YUV422P)
 
 
+class WebcamLineSensor(ObjectSensor):
+    """The webcam line sensor's codec instance (trik/webcam/line_sensor glue,
+    LineDetector<YUV422, RGB565X>): same quartet and InArgs/OutArgs as the
+    object sensor, packed YUYV input; process() uses only detectValFrom/To,
+    targetY is always 0, autoDetectHsv is ignored."""
+
+    _create = "TRIK_VIDTRANSCODE_CV_create_webcam_line"
+
+
 class BlobSensor(ObjectSensor):
     """The ov7670 object sensor's codec instance (trik/ov7670/object_sensor:
     BallDetector<YUV422P, RGB565X> with BitmapBuilder + Clusterizer): its own

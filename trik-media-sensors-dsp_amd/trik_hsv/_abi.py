@@ -168,6 +168,7 @@ PROTOTYPES = {
     "TRIK_VIDTRANSCODE_CV_create": ([C.POINTER(Params), C.POINTER(C.c_void_p)], i32),
     "TRIK_VIDTRANSCODE_CV_create_line": ([C.POINTER(Params), C.POINTER(C.c_void_p)], i32),
     "TRIK_VIDTRANSCODE_CV_create_ov7670": ([C.POINTER(Params), C.POINTER(C.c_void_p)], i32),
+    "TRIK_VIDTRANSCODE_CV_create_webcam_line": ([C.POINTER(Params), C.POINTER(C.c_void_p)], i32),
     "TRIK_VIDTRANSCODE_CV_delete": ([C.c_void_p], i32),
     # InArgs / OutArgs by pointer: the webcam structs, or the OV7670 ones for
     # a create_ov7670 handle (their base.size fields say which)
