@@ -68,7 +68,7 @@ constexpr int kQueueCap = 128;  // blob kernel, entries per wave: < 64 waiting +
 // queue down to < kDrainAt entries after every step, and a step appends its
 // words at once when they fit (else word by word, draining before each).
 constexpr int kHotLanes = 960;
-constexpr int kHotQueueCap = 59 + 128;  // what the LDS image leaves: 15 x 187 x 8 B
+constexpr int kHotQueueCap = 53 + 128;  // what the LDS image leaves: 15 x 181 x 8 B (+ 15 x 48 B of rare sums)
 // per-step appends drain full rounds of 64; word-by-word appends (A/B) drain at
 // 60 every second word, so the queue holds < 60 + 128 entries
 #ifndef TRIK_CHROMA_DRAIN_AT
@@ -96,7 +96,10 @@ static_assert(kLdsBlocks + 8192 <= kLdsPairs, "LDS layout");
 constexpr uint32_t kLdsBlkPair = kLdsBlocks;          // u8 [4096]
 constexpr uint32_t kLdsBlkCut = kLdsBlocks + 4096;    // u8 [4096]
 #endif
-constexpr uint32_t kLdsBytes = kLdsQueues + (kHotLanes / 64) * kHotQueueCap * 8;
+// per wave: the 12 u32 sums (3 per range) of the words the rare overflow
+// path resolved (drain_rare), added to the wave's sums at the tile end
+constexpr uint32_t kLdsRare = kLdsQueues + (kHotLanes / 64) * kHotQueueCap * 8;
+constexpr uint32_t kLdsBytes = kLdsRare + (kHotLanes / 64) * 48;
 static_assert(kLdsBytes <= 160 * 1024, "chroma kernel LDS image");
 
 typedef __attribute__((address_space(3))) uint8_t* lds8_t;
@@ -518,6 +521,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     for (int i = t; i < kChromaPalette; i += blockDim.x) st64(kLdsPairs + 8 * i, ct->palette[2 * i], ct->palette[2 * i + 1]);
     for (int i = t; i < 131072 / 16; i += blockDim.x)
       *(lds128_t)(uintptr_t)(kLdsRuns + 16 * i) = reinterpret_cast<const u32x4*>(ct->runs)[i];
+    for (int i = t; i < (kHotLanes / 64) * 12; i += blockDim.x) *(lds32_t)(uintptr_t)(kLdsRare + 4 * i) = 0u;
     for (int i = t; i < 256; i += blockDim.x) {
       *(lds16_t)(uintptr_t)(kLdsLut43 + 2 * i) = a.tables->lut43[i];
       *(lds16_t)(uintptr_t)(kLdsLut255 + 2 * i) = a.tables->lut255[i];
@@ -530,6 +534,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
 
   const int lane = t & 63;
   const uint32_t qbase_s = __builtin_amdgcn_readfirstlane(kLdsQueues + (uint32_t)(t >> 6) * (kHotQueueCap * 8));
+  const uint32_t rare_s = __builtin_amdgcn_readfirstlane(kLdsRare + (uint32_t)(t >> 6) * 48u);
   const bool active = t < g.k * g.cpr;
   const int col = active ? t % g.cpr : 0;
   const int ro = active ? t / g.cpr : 0;
@@ -590,22 +595,31 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     };
     // One drain round: lanes 0..take-1 resolve the last take queue entries
     // (two pixels each) exactly.
+    // The exact masks of the flagged pixels of queue entry qn - take + lane
+    // (which of the word's pixels the fast path left to this path: select2);
+    // verification mode writes them.
+    auto resolve = [&](int take, uint32_t& x, uint32_t& yr, uint32_t& m0, uint32_t& m1) {
+      const u32x2 ent = ld64(qbase_s + 8u * (uint32_t)(qn - take + lane));
+      const uint32_t w = ent.x;
+      x = ent.y & 0xFFFFu;
+      yr = ent.y >> 16;
+      const uint32_t d = ld16(kLdsRuns + 2u * chroma_of(w));
+      const uint32_t lo = d & 0xFFu, hi = d >> 8, Y0 = w & 0xFFu, Y1 = (w >> 16) & 0xFFu;
+      const bool xw = d == kChromaExc;
+      const bool f0 = xw | ((Y0 < lo) & (Y0 > hi)), f1 = xw | ((Y1 < lo) & (Y1 > hi));
+      m0 = f0 ? exact_mask<0>(w) : 0u;
+      m1 = f1 ? exact_mask<1>(w) : 0u;
+      if (MASKS) {
+        uint8_t* mp = a.masks + ((int64_t)f * a.height + r0 + yr) * a.width + x;
+        if (f0) mp[0] = a.mask_shift ? (uint8_t)(mp[0] | (m0 << a.mask_shift)) : (uint8_t)m0;
+        if (f1) mp[1] = a.mask_shift ? (uint8_t)(mp[1] | (m1 << a.mask_shift)) : (uint8_t)m1;
+      }
+    };
     auto drain = [&](int take) {
       if (lane < take) {
-        const u32x2 ent = ld64(qbase_s + 8u * (uint32_t)(qn - take + lane));
-        const uint32_t w = ent.x, x = ent.y & 0xFFFFu, yr = ent.y >> 16;
-        // which of the word's pixels the fast path left to this path (select2)
-        const uint32_t d = ld16(kLdsRuns + 2u * chroma_of(w));
-        const uint32_t lo = d & 0xFFu, hi = d >> 8, Y0 = w & 0xFFu, Y1 = (w >> 16) & 0xFFu;
-        const bool xw = d == kChromaExc;
-        const bool f0 = xw | ((Y0 < lo) & (Y0 > hi)), f1 = xw | ((Y1 < lo) & (Y1 > hi));
-        const uint32_t m0 = f0 ? exact_mask<0>(w) : 0u, m1 = f1 ? exact_mask<1>(w) : 0u;
+        uint32_t x, yr, m0, m1;
+        resolve(take, x, yr, m0, m1);
         const uint32_t e0 = spread4(m0), e1 = spread4(m1);
-        if (MASKS) {
-          uint8_t* mp = a.masks + ((int64_t)f * a.height + r0 + yr) * a.width + x;
-          if (f0) mp[0] = a.mask_shift ? (uint8_t)(mp[0] | (m0 << a.mask_shift)) : (uint8_t)m0;
-          if (f1) mp[1] = a.mask_shift ? (uint8_t)(mp[1] | (m1 << a.mask_shift)) : (uint8_t)m1;
-        }
         ex.EN += e0 + e1;
         const uint32_t a0 = e0 & 0x00FF00FFu, a1 = e1 & 0x00FF00FFu;
         const uint32_t b0 = (e0 >> 8) & 0x00FF00FFu, b1 = (e1 >> 8) & 0x00FF00FFu;
@@ -616,6 +630,37 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
       }
       if (++ex.rounds == g.flush_rounds) unpack_exc();
       __builtin_amdgcn_wave_barrier();  // the entries are read before the slots are reused
+      qn -= take;
+    };
+    // The same round for the rare overflow cases (a step whose words do not
+    // fit the queue): its sums go to the wave's LDS slots, not to the lane
+    // registers, so that the per-step path carries no second version of the
+    // lane sums (a register-merge copy of 17 values per step otherwise).
+    auto drain_rare = [&](int take) {
+      uint32_t v[12];
+#pragma unroll
+      for (int i = 0; i < 12; ++i) v[i] = 0u;
+      if (lane < take) {
+        uint32_t x, yr, m0, m1;
+        resolve(take, x, yr, m0, m1);
+        const uint32_t y = (uint32_t)r0 + yr;
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr) {
+          const uint32_t b0 = (m0 >> rr) & 1u, b1 = (m1 >> rr) & 1u;
+          v[3 * rr] = b0 + b1;
+          v[3 * rr + 1] = (b0 + b1) * x + b1;
+          v[3 * rr + 2] = (b0 + b1) * y;
+        }
+      }
+      wave_sums12(v);
+      if ((lane & 15) == 15 && (lane >> 4) < NR) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {  // one lane per slot: no atomics
+          const uint32_t ra = rare_s + 12u * (uint32_t)(lane >> 4) + 4u * i;
+          *(lds32_t)(uintptr_t)ra = *(lds32_t)(uintptr_t)ra + v[i];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
       qn -= take;
     };
 
@@ -720,7 +765,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         // first, and a step with more flagged words than the queue holds
         // (never seen) stores word by word, emptying it after each
         if (qn + total > kHotQueueCap)
-          while (qn > 0) drain(qn < 64 ? qn : 64);
+          while (qn > 0) drain_rare(qn < 64 ? qn : 64);
         if (total <= kHotQueueCap) {
           // entry index = the entries before this slot + the lane's rank (mbcnt
           // accumulates the scalar count; measured faster than a v_lshl_add on
@@ -735,11 +780,12 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
           }
           qn += total;
         } else {
+#pragma unroll
           for (int i = 0; i < CW; ++i) {
             const uint32_t qoff = __builtin_amdgcn_readfirstlane(qbase_s + 8u * (uint32_t)qn);
             store_masked(bal[i], qoff + 8u * rank(bal[i]), cw[i], (i < 4 ? pos_s : pos_b) + xoff(i));
             qn += __builtin_popcountll(bal[i]);
-            while (qn > 0) drain(qn < 64 ? qn : 64);
+            while (qn > 0) drain_rare(qn < 64 ? qn : 64);
           }
         }
 #ifdef TRIK_AB_NO_DRAIN  // timing attribution only (drops the exception words)
@@ -859,6 +905,15 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
       // lane 16 r + 15 holds values 3 r .. 3 r + 2: range r's N, sum x, sum y
       const int rr = lane >> 4;
       if (rr < NR) {
+#if TRIK_CHROMA_Q2
+        // and the rare path's sums of this tile
+        const uint32_t ra = rare_s + 12u * (uint32_t)rr;
+#pragma unroll
+        for (int v = 0; v < 3; ++v) {
+          red[v] += *(lds32_t)(uintptr_t)(ra + 4u * v);
+          *(lds32_t)(uintptr_t)(ra + 4u * v) = 0u;
+        }
+#endif
         unsigned long long* dst =
             reinterpret_cast<unsigned long long*>(&a.sums[(int64_t)f * a.sums_ranges + a.range_offset + rr].points);
 #pragma unroll
