@@ -24,6 +24,8 @@ SETS = {
                      (0, 359, 0, 100, 60, 65), (0, 359, 0, 100, 80, 85)],
     "four S bands": [(0, 359, 20, 25, 0, 100), (0, 359, 40, 45, 0, 100),
                      (0, 359, 60, 65, 0, 100), (0, 359, 80, 85, 0, 100)],
+    "one V range": [(0, 359, 0, 100, 30, 70)],
+    "S+V hue-free": [(0, 359, 30, 100, 20, 100), (0, 359, 0, 100, 60, 100)],
 }
 
 
@@ -44,16 +46,20 @@ def main():
             det.batch_sums(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, ranges, sums, stream=stream)
             if hot == trik_hsv.HOT_CHROMA:
                 line.append(f"flagged {det.chroma_flagged_share():.3f}")
+            for _ in range(10):  # the clocks ramp
+                det.batch_sums(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, ranges, sums, stream=stream)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            for _ in range(5):
+            for _ in range(20):
                 det.batch_sums(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, ranges, sums, stream=stream)
             e1.record(stream)
             torch.cuda.synchronize()
             ran = {trik_hsv.HOT_CHROMA: "chroma", trik_hsv.HOT_STRIPE: "stripe"}.get(det.last_hot_kernel(), "?")
+            ms = e0.elapsed_time(e1) / 20
+            frac = F * H * ll / (ms * 1e-3) / 8e12
             line.append(f"{['auto', 'stripe', 'chroma', 'generic'][hot] if hot < 4 else hot}->{ran} "
-                        f"{e0.elapsed_time(e1) / 5:.3f} ms")
+                        f"{ms:.3f} ms ({100 * frac:.1f} %)")
         det.close()
         print("  ".join(line), flush=True)
 

@@ -121,7 +121,11 @@ __device__ __forceinline__ uint32_t pack_bits(uint32_t e) {
   return ((e * 0x01020408u) >> 24) & 0xFu;  // bit 8t lands on bit 24+t
 }
 
-template <int LAYOUT, int NR, bool MASKS>
+// HUE = false: every range of the launch accepts every hue (KernelArgs::
+// hue_free; the S- and V-band sets), so detection is the sat&val mask alone:
+// no hue case select, no LUT43 or hue lookup (~15 instead of ~29 VALU per
+// pixel), and only the sv table is staged.
+template <int LAYOUT, int NR, bool MASKS, bool HUE>
 __global__ __launch_bounds__(kMaxBlock) __attribute__((amdgpu_waves_per_eu(8)))
 void stripe_kernel(KernelArgs a, StripeGeom g) {
   if (gated_out(a.gate, a.gate_max, a.gate_le)) return;
@@ -130,7 +134,8 @@ void stripe_kernel(KernelArgs a, StripeGeom g) {
     const u32x4* src = reinterpret_cast<const u32x4*>(a.stripe_tables);
     typedef __attribute__((address_space(3))) u32x4* lds_u128_wptr;
     lds_u128_wptr dst = (lds_u128_wptr)(uintptr_t)0;
-    for (int i = threadIdx.x; i < (int)(sizeof(StripeTables) / 16); i += blockDim.x) dst[i] = src[i];
+    constexpr int kStage = HUE ? (int)(sizeof(StripeTables) / 16) : (int)(sizeof(StripeTables::sv) / 16);
+    for (int i = threadIdx.x; i < kStage; i += blockDim.x) dst[i] = src[i];
   }
   __syncthreads();
 
@@ -192,13 +197,18 @@ void stripe_kernel(KernelArgs a, StripeGeom g) {
         p[1] = phase1<1>(w0, w0 ^ 0xFF00FF00u, m43_lane);
         p[2] = phase1<0>(w1, w1 ^ 0xFF00FF00u, m43_lane);
         p[3] = phase1<1>(w1, w1 ^ 0xFF00FF00u, m43_lane);
+        if constexpr (HUE) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          m[j] = lds_u32(p[j].m43_addr);
-          sv[j] = lds_u8(p[j].sv_addr);
+          for (int j = 0; j < 4; ++j) {
+            m[j] = lds_u32(p[j].m43_addr);
+            sv[j] = lds_u8(p[j].sv_addr);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) e[j] = combine(lds_u32(phase2_addr(m[j], p[j], hue_lane)), sv[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) e[j] = combine(0x01010101u, lds_u8(p[j].sv_addr));
         }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) e[j] = combine(lds_u32(phase2_addr(m[j], p[j], hue_lane)), sv[j]);
         if (MASKS && valid) {
           const int y = y0 + s * g.k;
           uint8_t* mp = a.masks + ((int64_t)f * a.height + y) * a.width + x0 + 4 * half;
@@ -301,9 +311,9 @@ bool geometry(const KernelArgs& a, StripeGeom& g, int64_t slots) {
   return true;
 }
 
-template <int LAYOUT, int NR, bool MASKS>
+template <int LAYOUT, int NR, bool MASKS, bool HUE>
 int launch_t(const KernelArgs& a, const StripeGeom& g, hipStream_t s) {
-  auto kern = stripe_kernel<LAYOUT, NR, MASKS>;
+  auto kern = stripe_kernel<LAYOUT, NR, MASKS, HUE>;
   {
     hipError_t e = set_dynamic_lds(reinterpret_cast<const void*>(kern), (int)kLdsStripe);
     if (e != hipSuccess) return e;
@@ -315,15 +325,20 @@ int launch_t(const KernelArgs& a, const StripeGeom& g, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int LAYOUT, bool MASKS>
+template <int LAYOUT, bool MASKS, bool HUE>
 int launch_nr(const KernelArgs& a, const StripeGeom& g, hipStream_t s) {
   switch (a.n_ranges) {
-    case 1: return launch_t<LAYOUT, 1, MASKS>(a, g, s);
-    case 2: return launch_t<LAYOUT, 2, MASKS>(a, g, s);
-    case 3: return launch_t<LAYOUT, 3, MASKS>(a, g, s);
-    case 4: return launch_t<LAYOUT, 4, MASKS>(a, g, s);
+    case 1: return launch_t<LAYOUT, 1, MASKS, HUE>(a, g, s);
+    case 2: return launch_t<LAYOUT, 2, MASKS, HUE>(a, g, s);
+    case 3: return launch_t<LAYOUT, 3, MASKS, HUE>(a, g, s);
+    case 4: return launch_t<LAYOUT, 4, MASKS, HUE>(a, g, s);
   }
   return hipErrorInvalidValue;
+}
+
+template <int LAYOUT, bool MASKS>
+int launch_hue(const KernelArgs& a, const StripeGeom& g, hipStream_t s) {
+  return a.hue_free ? launch_nr<LAYOUT, MASKS, false>(a, g, s) : launch_nr<LAYOUT, MASKS, true>(a, g, s);
 }
 
 }  // namespace
@@ -337,10 +352,10 @@ int launch_stripe(const KernelArgs& a, bool write_masks, hipStream_t s) {
     return hipErrorNotSupported;
   if (g.n_tiles == 0) return hipSuccess;
   if (a.layout == TRIK_HSV_LAYOUT_YUYV)
-    return write_masks ? launch_nr<TRIK_HSV_LAYOUT_YUYV, true>(a, g, s)
-                       : launch_nr<TRIK_HSV_LAYOUT_YUYV, false>(a, g, s);
-  return write_masks ? launch_nr<TRIK_HSV_LAYOUT_OV7670, true>(a, g, s)
-                     : launch_nr<TRIK_HSV_LAYOUT_OV7670, false>(a, g, s);
+    return write_masks ? launch_hue<TRIK_HSV_LAYOUT_YUYV, true>(a, g, s)
+                       : launch_hue<TRIK_HSV_LAYOUT_YUYV, false>(a, g, s);
+  return write_masks ? launch_hue<TRIK_HSV_LAYOUT_OV7670, true>(a, g, s)
+                     : launch_hue<TRIK_HSV_LAYOUT_OV7670, false>(a, g, s);
 }
 
 }  // namespace trik_hsv

@@ -84,6 +84,13 @@ void compile_stripe_tables(const RangeTables& base, int n, StripeTables* out) {
   }
 }
 
+bool hue_free(const RangeTables& t, int n) {
+  const uint8_t all = (uint8_t)((1u << (n < 4 ? n : 4)) - 1u);
+  for (int h = 0; h < 256; ++h)
+    if ((t.hue[h] & all) != all) return false;
+  return n > 0;
+}
+
 void preview_maps(int width, int height, int out_w, int out_h, uint32_t* maps, int col_lo, int col_hi) {
   // WSEQ:371-387: shift = min(out/in) in double, maps truncate i * shift
   const double sw = width > 0 ? (double)out_w / width : 0.0;
