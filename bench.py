@@ -150,7 +150,7 @@ def main():
     import torch.distributed as dist
 
     import trik_hsv
-    from trik_hsv.shard import all_reduce_totals, batch_totals, frame_shard
+    from trik_hsv.shard import all_reduce_totals, frame_shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -193,7 +193,7 @@ def main():
         if ev1 is not None:
             ev1.record(stream)
         targets = trik_hsv.batch_targets(sums, W, H, stream=stream)
-        totals = batch_totals(sums)
+        totals = trik_hsv.batch_totals_device(sums, stream=stream)  # totals_kernel (C ABI)
         if backend == "nccl":
             all_reduce_totals(totals)  # RCCL over xGMI when N > 1: 3*T int64 per step
         elif world > 1:  # gloo rehearsal: reduce a host copy
