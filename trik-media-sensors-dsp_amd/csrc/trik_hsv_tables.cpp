@@ -61,12 +61,24 @@ void compile_tables(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTa
       if (!outside(x, fs, ts)) out->smask[x] |= bit;
       if (!outside(x, fv, tv)) out->vmask[x] |= bit;
     }
-    for (uint32_t mx = 0; mx < 256; ++mx) {
-      if (outside(mx, fv, tv)) continue;
-      for (uint32_t mn = 0; mn <= mx; ++mn) {
-        const uint32_t s = (lut255[mx] * (mx - mn)) >> 8;
-        if (!outside(s, fs, ts)) out->sv[mx * 256 + mn] |= bit;
+    // S = (LUT255[mx] * d) >> 8 with d = mx - mn does not fall as d grows, so
+    // the d with fs <= S <= ts form one interval [d_lo, d_hi]: solved per mx
+    // instead of testing every (mx, mn) (a new range set is compiled on the
+    // host before its batch is enqueued)
+    for (uint32_t mx = fv; mx <= tv && mx < 256; ++mx) {
+      const uint32_t L = lut255[mx];
+      uint32_t d_lo, d_hi;
+      if (L == 0) {  // mx = 0: S = 0
+        if (fs > 0) continue;
+        d_lo = 0;
+        d_hi = mx;
+      } else {
+        d_lo = (256u * fs + L - 1) / L;          // the least d with L d >= 256 fs
+        d_hi = (256u * (ts + 1) - 1) / L;        // the largest d with L d < 256 (ts + 1)
+        if (d_hi > mx) d_hi = mx;
       }
+      uint8_t* row = out->sv + mx * 256;
+      for (uint32_t d = d_lo; d <= d_hi; ++d) row[mx - d] |= bit;
     }
   }
 }
