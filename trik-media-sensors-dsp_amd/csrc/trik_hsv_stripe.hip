@@ -191,13 +191,14 @@ void stripe_kernel(KernelArgs a, StripeGeom g) {
       // 4 pixels (words w0, w1) of row y0 + s*k at chunk pixel offset 4*half
       auto half_step = [&](uint32_t w0, uint32_t w1, int s, int half, uint32_t& Pa, uint32_t& Pb) {
         const bool valid = FULL || s < vsteps;
-        Phase1 p[4];
-        uint32_t m[4], sv[4], e[4];
-        p[0] = phase1<0>(w0, w0 ^ 0xFF00FF00u, m43_lane);
-        p[1] = phase1<1>(w0, w0 ^ 0xFF00FF00u, m43_lane);
-        p[2] = phase1<0>(w1, w1 ^ 0xFF00FF00u, m43_lane);
-        p[3] = phase1<1>(w1, w1 ^ 0xFF00FF00u, m43_lane);
+        uint32_t e[4];
         if constexpr (HUE) {
+          Phase1 p[4];
+          uint32_t m[4], sv[4];
+          p[0] = phase1<0>(w0, w0 ^ 0xFF00FF00u, m43_lane);
+          p[1] = phase1<1>(w0, w0 ^ 0xFF00FF00u, m43_lane);
+          p[2] = phase1<0>(w1, w1 ^ 0xFF00FF00u, m43_lane);
+          p[3] = phase1<1>(w1, w1 ^ 0xFF00FF00u, m43_lane);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             m[j] = lds_u32(p[j].m43_addr);
@@ -206,8 +207,12 @@ void stripe_kernel(KernelArgs a, StripeGeom g) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) e[j] = combine(lds_u32(phase2_addr(m[j], p[j], hue_lane)), sv[j]);
         } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) e[j] = combine(0x01010101u, lds_u8(p[j].sv_addr));
+          const uint32_t a0 = sv_addr_only<0>(w0, w0 ^ 0xFF00FF00u), a1 = sv_addr_only<1>(w0, w0 ^ 0xFF00FF00u);
+          const uint32_t a2 = sv_addr_only<0>(w1, w1 ^ 0xFF00FF00u), a3 = sv_addr_only<1>(w1, w1 ^ 0xFF00FF00u);
+          e[0] = combine(0x01010101u, lds_u8(a0));
+          e[1] = combine(0x01010101u, lds_u8(a1));
+          e[2] = combine(0x01010101u, lds_u8(a2));
+          e[3] = combine(0x01010101u, lds_u8(a3));
         }
         if (MASKS && valid) {
           const int y = y0 + s * g.k;

@@ -70,6 +70,21 @@ __device__ __forceinline__ Phase1 phase1(uint32_t w, uint32_t wc, uint32_t m43_l
   return p;
 }
 
+// The sat&val table address alone (ranges that accept every hue): clamp8 is
+// monotone, so max and min of the clamped channels are the clamped max and min
+// of the unclamped ones (two clamps per pixel instead of three).
+template <int PIX>
+__device__ __forceinline__ uint32_t sv_addr_only(uint32_t w, uint32_t wc) {
+  constexpr uint32_t kY = PIX == 0 ? 74u : (74u << 16);
+  auto shift6 = [](uint32_t s) { return ((int)(s << 16)) >> 22; };  // v_bfe_i32 s, 6, 10
+  const int r = shift6(__builtin_amdgcn_udot4(w, kY | (102u << 24), (uint32_t)-14248, false));
+  const int g = shift6(__builtin_amdgcn_udot4(wc, kY | (25u << 8) | (52u << 24), (uint32_t)-10939, false));
+  const int b = shift6(__builtin_amdgcn_udot4(w, kY | (129u << 8), (uint32_t)-17672, false));
+  const int mx = min(max(max(r, max(g, b)), 0), 255);
+  const int mn = min(max(min(r, min(g, b)), 0), 255);
+  return __umul24((uint32_t)mx, (uint32_t)kSvStride) + (uint32_t)mn;
+}
+
 // Phase 2: h = base + m * diff (WSEQ:226-246; m < 2^14, |diff| < 2^8, so one
 // v_mad_i32_i24), whose bits 15:8 (H) select the byte-spread hue mask (range t
 // -> bit 8t); returns the LDS byte address of this lane's copy.
