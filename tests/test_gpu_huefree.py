@@ -1,10 +1,12 @@
-"""GPU parity of the stripe kernel's hue-free form (trik_hsv_stripe.hip,
-HUE = false): range groups whose every range accepts every hue (H 0..359 --
-the S- and V-band sets, the webcam line sensor's V-only range) are detected by
-the sat&val table alone.  Bit-exact against the oracle (detectHsvPixel,
-WSEQ:171-179, with the hue lane always inside) on every (Y,U,V) triple, in
-both layouts, and on batches; mixed groups (one range with a hue bound) keep
-the full kernel and are checked the same way.
+"""GPU parity of the stripe kernel's reduced detection forms
+(trik_hsv_stripe.hip, detect_mode): range groups whose every range accepts
+every hue (H 0..359 -- the S-band sets) are detected by the sat&val table
+alone (kDetectSV), and groups that also accept every saturation (V bands, the
+webcam line sensor's range) by the value test alone (kDetectV).  Bit-exact
+against the oracle (detectHsvPixel, WSEQ:171-179, with the hue lane always
+inside) on every (Y,U,V) triple, in both layouts, and on batches; mixed
+groups (one range with a hue bound) keep the full kernel and are checked the
+same way.
 """
 import numpy as np
 import pytest
@@ -21,9 +23,14 @@ HUE_FREE_EDGE = [(0, 359, 0, 100, 0, 100),   # everything
                  (0, 359, 0, 0, 0, 100),     # grey only
                  (0, 359, 0, 100, 0, 10),    # dark only
                  (0, 359, 100, 100, 100, 100)]  # one S, V point
-SETS = {"s_bands": S_BANDS, "v_bands": V_BANDS, "edge": HUE_FREE_EDGE,
+V_EDGE = [(0, 359, 0, 100, 0, 0),      # V = 0 only
+          (0, 359, 0, 100, 100, 100),  # V = 255 only
+          (0, 359, -5, 120, -10, 3),   # clamped arguments
+          (0, 359, 0, 100, 99, 120)]
+SETS = {"s_bands": S_BANDS, "v_bands": V_BANDS, "edge": HUE_FREE_EDGE, "v_edge": V_EDGE,
         "one_v": [(0, 359, 0, 100, 30, 70)], "two_s": S_BANDS[:2],
         "mixed": [S_BANDS[0], T0, V_BANDS[1]]}
+V_ONLY = ("v_bands", "v_edge", "one_v")
 
 
 @pytest.fixture(scope="module")
@@ -76,6 +83,8 @@ def test_exhaustive_hue_free(torch_dev, stripe, oracle_mod, name, layout):
     ("s_bands", 640, 480, LAYOUT_YUYV, 24),
     ("v_bands", 640, 480, LAYOUT_YUYV, 24),
     ("one_v", 1280, 720, LAYOUT_YUYV, 6),
+    ("one_v", 640, 480, LAYOUT_YUYV, 40),                  # AUTO: the value form at a large batch
+    ("v_edge", 640, 480, LAYOUT_YUYV, 8),
     ("v_bands", 320, 240, LAYOUT_OV7670, 16),
     ("mixed", 640, 480, LAYOUT_YUYV, 8),
 ])
@@ -98,5 +107,7 @@ def test_batches_hue_free(torch_dev, oracle_mod, name, w, h, layout, n, kind):
             sums, tg = d.process_batch(dev, w, h, ll, layout, ranges)
             assert np.array_equal(sums.cpu().numpy(), want_s), (hot, name)
             assert np.array_equal(tg[:, :, :3].cpu().numpy(), want_t), (hot, name)
+            if name in V_ONLY:  # AUTO keeps value-only groups on the stripe kernel at any size
+                assert d.last_hot_kernel() == trik_hsv.HOT_STRIPE
         finally:
             d.close()

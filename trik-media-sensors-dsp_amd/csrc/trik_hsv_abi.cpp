@@ -194,7 +194,7 @@ struct TableSet {
   StripeTables* h_stripe = nullptr;
   ChromaTables* d_chroma = nullptr;        // built on first use per range set (chroma-run kernel)
   unsigned long long* h_cost = nullptr;    // pinned readback of each group's flagged_cost
-  std::vector<uint8_t> hue_free;           // per group: every range accepts every hue
+  std::vector<uint8_t> detect;             // per group: detect_mode() of its ranges
   bool chroma_built = false;
   double chroma_share = -1.0;  // the builder's expected exact-path word share (max over groups), once read
   hipEvent_t ready = nullptr;       // uploads (and the chroma build) enqueued before it
@@ -437,10 +437,10 @@ int32_t acquire_tables(TrikCvHandle* h, const TRIK_VIDTRANSCODE_CV_InArgsAlg* ra
     compile_tables(ranges + g * kRangesPerLaunch, cnt, &v->h_tables[g]);
     compile_stripe_tables(v->h_tables[g], cnt, &v->h_stripe[g]);
   }
-  v->hue_free.assign(groups, 0);
+  v->detect.assign(groups, kDetectFull);
   for (int g = 0; g < groups; ++g) {
     const int cnt = n - g * kRangesPerLaunch < kRangesPerLaunch ? n - g * kRangesPerLaunch : kRangesPerLaunch;
-    v->hue_free[g] = hue_free(v->h_tables[g], cnt) ? 1 : 0;
+    v->detect[g] = (uint8_t)detect_mode(v->h_tables[g], cnt);
   }
   HIP_TRY(hipMemcpyAsync(v->d_tables, v->h_tables, sizeof(RangeTables) * groups, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(v->d_stripe, v->h_stripe, sizeof(StripeTables) * groups, hipMemcpyHostToDevice, s));
@@ -513,14 +513,17 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
     a.sums_ranges = n;
     a.tables = t->d_tables + g;
     a.stripe_tables = t->d_stripe + g;
-    a.hue_free = t->hue_free[g];
+    a.detect_mode = t->detect[g];
     a.sums = sums;
     a.masks = masks;
     a.mask_shift = g * kRangesPerLaunch;
     // the chroma-run kernel for large batches, the stripe kernel otherwise;
     // the generic kernel takes misaligned inputs and rows wider than 8192 pixels
-    const HotPlan plan = plan_hot(h, *t, groups, big, h->hot.load() != TRIK_HSV_HOT_GENERIC && chroma_geometry_ok(a),
-                                  s, &rc);
+    // value-only groups (every range accepts every hue and saturation) run
+    // the stripe kernel's value form under AUTO at any batch size: it beats
+    // the chroma-run kernel there and needs no table build
+    const HotPlan plan = plan_hot(h, *t, groups, big && t->detect[g] != kDetectV,
+                                  h->hot.load() != TRIK_HSV_HOT_GENERIC && chroma_geometry_ok(a), s, &rc);
     if (rc) return rc;
     int e = hipErrorNotSupported;
     if (plan == kPlanChroma) {

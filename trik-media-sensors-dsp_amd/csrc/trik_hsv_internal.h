@@ -101,8 +101,11 @@ struct alignas(16) ChromaTables {
 PackedRange pack_range(const TRIK_VIDTRANSCODE_CV_InArgsAlg& r);
 void compile_tables(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTables* out);
 void compile_stripe_tables(const RangeTables& base, int n, StripeTables* out);
-// true when each of the n ranges compiled into t accepts every hue value
-bool hue_free(const RangeTables& t, int n);
+// Which tests of detectHsvPixel (WSEQ:171-179) a group of n compiled ranges
+// needs: kDetectFull; kDetectSV when each accepts every hue value; kDetectV
+// when each also accepts every saturation value.
+enum DetectMode { kDetectFull = 0, kDetectSV = 1, kDetectV = 2 };
+int detect_mode(const RangeTables& t, int n);
 
 struct KernelArgs {
   const uint8_t* frames;
@@ -118,9 +121,10 @@ struct KernelArgs {
   TrikHsvTargetSums* sums;
   uint8_t* masks;        // verification mode only
   int32_t mask_shift;    // bit position of this launch's range 0 in the mask byte
-  // every range of this launch accepts every hue (RangeTables::hue all ones
-  // for its n_ranges bits): the stripe kernel skips the hue arithmetic
-  int32_t hue_free = 0;
+  // the detection the stripe kernel needs for this group (detect_mode()):
+  // kDetectSV when every range accepts every hue, kDetectV when every range
+  // also accepts every saturation
+  int32_t detect_mode = 0;
   // Device-side kernel choice while the host does not know a new range set's
   // exact-path share yet: with gate set the kernel runs only if
   // (*gate <= gate_max) == gate_le (one uniform load per workgroup).

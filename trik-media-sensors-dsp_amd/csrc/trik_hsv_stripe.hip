@@ -121,11 +121,19 @@ __device__ __forceinline__ uint32_t pack_bits(uint32_t e) {
   return ((e * 0x01020408u) >> 24) & 0xFu;  // bit 8t lands on bit 24+t
 }
 
-// HUE = false: every range of the launch accepts every hue (KernelArgs::
-// hue_free; the S- and V-band sets), so detection is the sat&val mask alone:
-// no hue case select, no LUT43 or hue lookup (~15 instead of ~29 VALU per
-// pixel), and only the sv table is staged.
-template <int LAYOUT, int NR, bool MASKS, bool HUE>
+// MODE (KernelArgs::detect_mode): the detection a launch group needs.
+//  kDetectFull  the full pixel path above.
+//  kDetectSV    every range accepts every hue (the S- and V-band sets): the
+//               sat&val mask alone -- no hue case select, no LUT43 or hue
+//               lookup (~15 instead of ~29 VALU per pixel); only sv is staged.
+//  kDetectV     every range also accepts every saturation (V bands, the webcam
+//               line sensor): the value test alone.  V = clamp8(max(R', G', B')
+//               >> 6) over the unclamped presums (clamp8 and >>6 are monotone;
+//               R', G' lie in int16, B' is the reference's 16-bit wrap), read
+//               from a 1024-entry byte-spread table indexed by (m >> 6) + 512
+//               whose ends hold the clamped values (~8 VALU per pixel); the
+//               table is built in LDS from RangeTables::vmask.
+template <int LAYOUT, int NR, bool MASKS, int MODE>
 __global__ __launch_bounds__(kMaxBlock) __attribute__((amdgpu_waves_per_eu(8)))
 void stripe_kernel(KernelArgs a, StripeGeom g) {
   if (gated_out(a.gate, a.gate_max, a.gate_le)) return;
@@ -134,8 +142,17 @@ void stripe_kernel(KernelArgs a, StripeGeom g) {
     const u32x4* src = reinterpret_cast<const u32x4*>(a.stripe_tables);
     typedef __attribute__((address_space(3))) u32x4* lds_u128_wptr;
     lds_u128_wptr dst = (lds_u128_wptr)(uintptr_t)0;
-    constexpr int kStage = HUE ? (int)(sizeof(StripeTables) / 16) : (int)(sizeof(StripeTables::sv) / 16);
-    for (int i = threadIdx.x; i < kStage; i += blockDim.x) dst[i] = src[i];
+    if constexpr (MODE == kDetectV) {
+      typedef __attribute__((address_space(3))) uint32_t* lds_u32_wptr;
+      const uint32_t keep = (1u << NR) - 1u;
+      for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+        const int v = i < 512 ? 0 : (i > 767 ? 255 : i - 512);
+        ((lds_u32_wptr)(uintptr_t)0)[i] = combine(0x01010101u, a.tables->vmask[v] & keep);
+      }
+    } else {
+      constexpr int kStage = MODE == kDetectFull ? (int)(sizeof(StripeTables) / 16) : (int)(sizeof(StripeTables::sv) / 16);
+      for (int i = threadIdx.x; i < kStage; i += blockDim.x) dst[i] = src[i];
+    }
   }
   __syncthreads();
 
@@ -192,7 +209,7 @@ void stripe_kernel(KernelArgs a, StripeGeom g) {
       auto half_step = [&](uint32_t w0, uint32_t w1, int s, int half, uint32_t& Pa, uint32_t& Pb) {
         const bool valid = FULL || s < vsteps;
         uint32_t e[4];
-        if constexpr (HUE) {
+        if constexpr (MODE == kDetectFull) {
           Phase1 p[4];
           uint32_t m[4], sv[4];
           p[0] = phase1<0>(w0, w0 ^ 0xFF00FF00u, m43_lane);
@@ -206,6 +223,11 @@ void stripe_kernel(KernelArgs a, StripeGeom g) {
           }
 #pragma unroll
           for (int j = 0; j < 4; ++j) e[j] = combine(lds_u32(phase2_addr(m[j], p[j], hue_lane)), sv[j]);
+        } else if constexpr (MODE == kDetectV) {
+          e[0] = lds_u32(v_addr<0>(w0, w0 ^ 0xFF00FF00u));
+          e[1] = lds_u32(v_addr<1>(w0, w0 ^ 0xFF00FF00u));
+          e[2] = lds_u32(v_addr<0>(w1, w1 ^ 0xFF00FF00u));
+          e[3] = lds_u32(v_addr<1>(w1, w1 ^ 0xFF00FF00u));
         } else {
           const uint32_t a0 = sv_addr_only<0>(w0, w0 ^ 0xFF00FF00u), a1 = sv_addr_only<1>(w0, w0 ^ 0xFF00FF00u);
           const uint32_t a2 = sv_addr_only<0>(w1, w1 ^ 0xFF00FF00u), a3 = sv_addr_only<1>(w1, w1 ^ 0xFF00FF00u);
@@ -316,9 +338,9 @@ bool geometry(const KernelArgs& a, StripeGeom& g, int64_t slots) {
   return true;
 }
 
-template <int LAYOUT, int NR, bool MASKS, bool HUE>
+template <int LAYOUT, int NR, bool MASKS, int MODE>
 int launch_t(const KernelArgs& a, const StripeGeom& g, hipStream_t s) {
-  auto kern = stripe_kernel<LAYOUT, NR, MASKS, HUE>;
+  auto kern = stripe_kernel<LAYOUT, NR, MASKS, MODE>;
   {
     hipError_t e = set_dynamic_lds(reinterpret_cast<const void*>(kern), (int)kLdsStripe);
     if (e != hipSuccess) return e;
@@ -330,20 +352,24 @@ int launch_t(const KernelArgs& a, const StripeGeom& g, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int LAYOUT, bool MASKS, bool HUE>
+template <int LAYOUT, bool MASKS, int MODE>
 int launch_nr(const KernelArgs& a, const StripeGeom& g, hipStream_t s) {
   switch (a.n_ranges) {
-    case 1: return launch_t<LAYOUT, 1, MASKS, HUE>(a, g, s);
-    case 2: return launch_t<LAYOUT, 2, MASKS, HUE>(a, g, s);
-    case 3: return launch_t<LAYOUT, 3, MASKS, HUE>(a, g, s);
-    case 4: return launch_t<LAYOUT, 4, MASKS, HUE>(a, g, s);
+    case 1: return launch_t<LAYOUT, 1, MASKS, MODE>(a, g, s);
+    case 2: return launch_t<LAYOUT, 2, MASKS, MODE>(a, g, s);
+    case 3: return launch_t<LAYOUT, 3, MASKS, MODE>(a, g, s);
+    case 4: return launch_t<LAYOUT, 4, MASKS, MODE>(a, g, s);
   }
   return hipErrorInvalidValue;
 }
 
 template <int LAYOUT, bool MASKS>
 int launch_hue(const KernelArgs& a, const StripeGeom& g, hipStream_t s) {
-  return a.hue_free ? launch_nr<LAYOUT, MASKS, false>(a, g, s) : launch_nr<LAYOUT, MASKS, true>(a, g, s);
+  switch (a.detect_mode) {
+    case kDetectSV: return launch_nr<LAYOUT, MASKS, kDetectSV>(a, g, s);
+    case kDetectV: return launch_nr<LAYOUT, MASKS, kDetectV>(a, g, s);
+  }
+  return launch_nr<LAYOUT, MASKS, kDetectFull>(a, g, s);
 }
 
 }  // namespace

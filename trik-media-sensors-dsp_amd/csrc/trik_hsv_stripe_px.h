@@ -85,6 +85,20 @@ __device__ __forceinline__ uint32_t sv_addr_only(uint32_t w, uint32_t wc) {
   return __umul24((uint32_t)mx, (uint32_t)kSvStride) + (uint32_t)mn;
 }
 
+// The value-only table address (ranges that accept every hue and every
+// saturation): m = max(R', G', sext16(B')) of the unclamped presums,
+// 4 * ((m >> 6) + 512) into a table of 1024 byte-spread value masks whose
+// entries below 512 / above 767 hold V = 0 / V = 255 (the clamp).
+template <int PIX>
+__device__ __forceinline__ uint32_t v_addr(uint32_t w, uint32_t wc) {
+  constexpr uint32_t kY = PIX == 0 ? 74u : (74u << 16);
+  const int r = (int)__builtin_amdgcn_udot4(w, kY | (102u << 24), (uint32_t)-14248, false);  // int16 range
+  const int g = (int)__builtin_amdgcn_udot4(wc, kY | (25u << 8) | (52u << 24), (uint32_t)-10939, false);
+  const int b = ((int)(__builtin_amdgcn_udot4(w, kY | (129u << 8), (uint32_t)-17672, false) << 16)) >> 16;
+  const int m = max(r, max(g, b));
+  return (uint32_t)(((m >> 6) + 512) << 2);
+}
+
 // Phase 2: h = base + m * diff (WSEQ:226-246; m < 2^14, |diff| < 2^8, so one
 // v_mad_i32_i24), whose bits 15:8 (H) select the byte-spread hue mask (range t
 // -> bit 8t); returns the LDS byte address of this lane's copy.

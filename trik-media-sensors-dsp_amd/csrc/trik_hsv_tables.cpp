@@ -96,11 +96,14 @@ void compile_stripe_tables(const RangeTables& base, int n, StripeTables* out) {
   }
 }
 
-bool hue_free(const RangeTables& t, int n) {
+int detect_mode(const RangeTables& t, int n) {
   const uint8_t all = (uint8_t)((1u << (n < 4 ? n : 4)) - 1u);
+  if (n <= 0) return kDetectFull;
   for (int h = 0; h < 256; ++h)
-    if ((t.hue[h] & all) != all) return false;
-  return n > 0;
+    if ((t.hue[h] & all) != all) return kDetectFull;
+  for (int x = 0; x < 256; ++x)
+    if ((t.smask[x] & all) != all) return kDetectSV;
+  return kDetectV;
 }
 
 void preview_maps(int width, int height, int out_w, int out_h, uint32_t* maps, int col_lo, int col_hi) {
