@@ -87,6 +87,9 @@ def test_exhaustive_hue_free(torch_dev, stripe, oracle_mod, name, layout):
     ("v_edge", 640, 480, LAYOUT_YUYV, 8),
     ("v_bands", 320, 240, LAYOUT_OV7670, 16),
     ("mixed", 640, 480, LAYOUT_YUYV, 8),
+    ("v_edge", 32, 4, LAYOUT_YUYV, 16),                    # minimal frames: partial tiles
+    ("s_bands", 8192, 8, LAYOUT_YUYV, 2),                  # the widest rows the stripe kernel takes
+    ("v_bands", 96, 12, LAYOUT_OV7670, 5),
 ])
 @pytest.mark.parametrize("kind", [0, 1])
 def test_batches_hue_free(torch_dev, oracle_mod, name, w, h, layout, n, kind):
