@@ -317,44 +317,54 @@ __global__ __launch_bounds__(256) void chroma_block_kernel(ChromaTables* ct) {
   if (t == 0) {
     best = ~0ull;
     n_pairs = 0;
-  }
-  __syncthreads();
-  if (t == 0) {  // the cuts: 0, then each chroma's first nonzero Y in (0, 255]
-    uint32_t n = 0;
-    cuts[n++] = 0;
-    for (int j = 0; j < 16; ++j)
-      if (fz[j] != 0u && fz[j] <= 255u) cuts[n++] = fz[j];
-    n_cuts = n;
-  }
-  {  // the pairs: thread t stands for pair k = t
-    const uint32_t k = t;
-    bool take;
+    // the palette pass: when this block's unrestricted choice (pass 1) made
+    // the palette, it is also the cheapest palette choice (the same keys over
+    // a subset that contains it) -- no second search
     if (PALETTE) {
-      take = ct->palette_of[k] != 0xFFu;
-    } else {
-      uint32_t present = 1u;  // mask values appearing (value 0 always a candidate)
-      for (int i = 0; i < 16; ++i) {
-        if (sf[i] & 3u) present |= 1u << ((sf[i] >> 4) & 15u);
-        if ((sf[i] & 3u) == 2u) present |= 1u << ((sf[i] >> 8) & 15u);
-        if (sd[i] & 3u) present |= 1u << ((sd[i] >> 4) & 15u);
-        if ((sd[i] & 3u) == 2u) present |= 1u << ((sd[i] >> 8) & 15u);
-      }
-      take = ((present >> (k & 15u)) & 1u) && ((present >> (k >> 4)) & 1u);
+      const unsigned long long b1 = ct->best[b];
+      if (ct->palette_of[(uint32_t)(b1 >> 9) & 255u] != 0xFFu) best = b1;
     }
-    if (take) pairs[atomicAdd(&n_pairs, 1u)] = k;  // order does not matter: the key decides
   }
   __syncthreads();
-  const uint32_t np = n_pairs, nc = n_cuts;
-  unsigned long long mine = ~0ull;
-  for (uint32_t combo = t; combo < np * nc; combo += blockDim.x) {
-    const uint32_t k = pairs[combo / nc], A = cuts[combo % nc];
-    uint32_t cost = 0;
-    for (int i = 0; i < 16; ++i) cost += chroma_cost(chroma_desc_cut(sf[i], sd[i], fz[i], k, A));
-    const unsigned long long key = ((unsigned long long)cost << 17) | ((unsigned long long)k << 9) | A;
-    if (key < mine) mine = key;
+  const bool known = PALETTE && best != ~0ull;  // uniform across the block
+  if (!known) {
+    if (t == 0) {  // the cuts: 0, then each chroma's first nonzero Y in (0, 255]
+      uint32_t n = 0;
+      cuts[n++] = 0;
+      for (int j = 0; j < 16; ++j)
+        if (fz[j] != 0u && fz[j] <= 255u) cuts[n++] = fz[j];
+      n_cuts = n;
+    }
+    {  // the pairs: thread t stands for pair k = t
+      const uint32_t k = t;
+      bool take;
+      if (PALETTE) {
+        take = ct->palette_of[k] != 0xFFu;
+      } else {
+        uint32_t present = 1u;  // mask values appearing (value 0 always a candidate)
+        for (int i = 0; i < 16; ++i) {
+          if (sf[i] & 3u) present |= 1u << ((sf[i] >> 4) & 15u);
+          if ((sf[i] & 3u) == 2u) present |= 1u << ((sf[i] >> 8) & 15u);
+          if (sd[i] & 3u) present |= 1u << ((sd[i] >> 4) & 15u);
+          if ((sd[i] & 3u) == 2u) present |= 1u << ((sd[i] >> 8) & 15u);
+        }
+        take = ((present >> (k & 15u)) & 1u) && ((present >> (k >> 4)) & 1u);
+      }
+      if (take) pairs[atomicAdd(&n_pairs, 1u)] = k;  // order does not matter: the key decides
+    }
+    __syncthreads();
+    const uint32_t np = n_pairs, nc = n_cuts;
+    unsigned long long mine = ~0ull;
+    for (uint32_t combo = t; combo < np * nc; combo += blockDim.x) {
+      const uint32_t k = pairs[combo / nc], A = cuts[combo % nc];
+      uint32_t cost = 0;
+      for (int i = 0; i < 16; ++i) cost += chroma_cost(chroma_desc_cut(sf[i], sd[i], fz[i], k, A));
+      const unsigned long long key = ((unsigned long long)cost << 17) | ((unsigned long long)k << 9) | A;
+      if (key < mine) mine = key;
+    }
+    if (mine != ~0ull) atomicMin(&best, mine);
+    __syncthreads();
   }
-  if (mine != ~0ull) atomicMin(&best, mine);
-  __syncthreads();
   const uint32_t bk = (uint32_t)(best >> 9) & 255u, bA = (uint32_t)best & 511u;
   if (!PALETTE) {
     if (t == 0) {
