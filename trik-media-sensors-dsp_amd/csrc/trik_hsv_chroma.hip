@@ -368,15 +368,14 @@ __global__ __launch_bounds__(256) void chroma_block_kernel(ChromaTables* ct) {
   const uint32_t bk = (uint32_t)(best >> 9) & 255u, bA = (uint32_t)best & 511u;
   if (!PALETTE) {
     if (t == 0) {
-      ct->best[b] = best;
-      atomicAdd(&ct->pair_hist[bk], 1u);
+      ct->best[b] = best;  // chroma_palette_kernel histograms the pairs
     }
     return;
   }
   if (t < 16) ct->runs[c0 + t] = (uint16_t)chroma_desc_cut(sf[t], sd[t], fz[t], bk, bA);
   if (t == 0) {
     ct->blocks[b] = (uint16_t)(ct->palette_of[bk] | (bA << 8));
-    atomicAdd(&ct->flagged_cost, best >> 17);
+    ct->block_cost[b] = (uint32_t)(best >> 17);  // summed by chroma_cost_kernel (no same-address atomics)
   }
 }
 
@@ -384,11 +383,17 @@ __global__ __launch_bounds__(256) void chroma_block_kernel(ChromaTables* ct) {
 // pairs (ties: the smaller k); palette_of[k] = 8 * slot or 0xFF, and the
 // byte-spread pair of each slot.
 __global__ __launch_bounds__(256) void chroma_palette_kernel(ChromaTables* ct) {
+  __shared__ uint32_t hist[256];
   const uint32_t k = threadIdx.x;
-  const uint32_t n = ct->pair_hist[k];
+  hist[k] = 0;
+  __syncthreads();
+  for (uint32_t b = k; b < 4096; b += 256) atomicAdd(&hist[(uint32_t)(ct->best[b] >> 9) & 255u], 1u);
+  __syncthreads();
+  const uint32_t n = hist[k];
+  ct->pair_hist[k] = n;
   uint32_t rank = 0;
   for (uint32_t j = 0; j < 256; ++j) {
-    const uint32_t m = ct->pair_hist[j];
+    const uint32_t m = hist[j];
     rank += (m > n) | ((m == n) & (j < k));
   }
   const bool in = n > 0 && rank < (uint32_t)kChromaPalette;
@@ -396,6 +401,23 @@ __global__ __launch_bounds__(256) void chroma_palette_kernel(ChromaTables* ct) {
   if (in) {
     ct->palette[2 * rank] = spread4(k & 15u);
     ct->palette[2 * rank + 1] = spread4(k >> 4);
+  }
+}
+
+// One workgroup of 1024: flagged_cost = the sum of the blocks' costs.
+__global__ __launch_bounds__(1024) void chroma_cost_kernel(ChromaTables* ct) {
+  __shared__ unsigned long long part[16];
+  const uint32_t t = threadIdx.x;
+  unsigned long long v = 0;
+  for (uint32_t b = t; b < 4096; b += 1024) v += ct->block_cost[b];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  if ((t & 63) == 0) part[t >> 6] = v;
+  __syncthreads();
+  if (t == 0) {
+    unsigned long long sum = 0;
+    for (int i = 0; i < 16; ++i) sum += part[i];
+    ct->flagged_cost = sum;
   }
 }
 
@@ -1098,13 +1120,10 @@ int build_chroma_tables(const RangeTables* t, ChromaTables* ct, hipStream_t s) {
   hipLaunchKernelGGL(chroma_summary_kernel, dim3(1024), dim3(256), 0, s, t, ct);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  e = hipMemsetAsync(ct->pair_hist, 0, sizeof(ct->pair_hist), s);
-  if (e != hipSuccess) return e;
-  e = hipMemsetAsync(&ct->flagged_cost, 0, sizeof(ct->flagged_cost), s);
-  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(chroma_block_kernel<false>, dim3(4096), dim3(256), 0, s, ct);
   hipLaunchKernelGGL(chroma_palette_kernel, dim3(1), dim3(256), 0, s, ct);
   hipLaunchKernelGGL(chroma_block_kernel<true>, dim3(4096), dim3(256), 0, s, ct);
+  hipLaunchKernelGGL(chroma_cost_kernel, dim3(1), dim3(1024), 0, s, ct);
   return hipGetLastError();
 }
 

@@ -80,7 +80,8 @@ constexpr uint32_t kChromaExc = 0x00FFu;  // b1 = 255, b2 = 0: the builder never
 //   summary / summary_drop / first_nz : builder scratch, per chroma: the run
 //                 summary of the profile from Y = 0 and from its first nonzero
 //                 Y on, and that Y (256: all zero); best[b]: the block's
-//                 packed (cost, pair, cut) choice
+//                 packed (cost, pair, cut) choice; block_cost[b]: its cost
+//                 after the palette pass
 constexpr int kChromaPalette = 32;  // 8 x slot fits the block byte
 struct alignas(16) ChromaTables {
   uint16_t runs[65536];
@@ -89,6 +90,7 @@ struct alignas(16) ChromaTables {
   uint32_t summary_drop[65536];
   uint16_t first_nz[65536];
   unsigned long long best[4096];
+  uint32_t block_cost[4096];  // the palette pass's cost per block (summed by chroma_cost_kernel)
   uint32_t pair_hist[256];
   uint32_t palette[2 * kChromaPalette];
   uint8_t palette_of[256];
