@@ -432,14 +432,11 @@ int32_t acquire_tables(TrikCvHandle* h, const TRIK_VIDTRANSCODE_CV_InArgsAlg* ra
   v->key.clear();  // invalid until the uploads are enqueued
   // the set's earlier uploads and readers have finished (idle), so its pinned
   // staging and device tables may be rewritten
+  v->detect.assign(groups, kDetectFull);
   for (int g = 0; g < groups; ++g) {
     const int cnt = n - g * kRangesPerLaunch < kRangesPerLaunch ? n - g * kRangesPerLaunch : kRangesPerLaunch;
     compile_tables(ranges + g * kRangesPerLaunch, cnt, &v->h_tables[g]);
     compile_stripe_tables(v->h_tables[g], cnt, &v->h_stripe[g]);
-  }
-  v->detect.assign(groups, kDetectFull);
-  for (int g = 0; g < groups; ++g) {
-    const int cnt = n - g * kRangesPerLaunch < kRangesPerLaunch ? n - g * kRangesPerLaunch : kRangesPerLaunch;
     v->detect[g] = (uint8_t)detect_mode(v->h_tables[g], cnt);
   }
   HIP_TRY(hipMemcpyAsync(v->d_tables, v->h_tables, sizeof(RangeTables) * groups, hipMemcpyHostToDevice, s));
