@@ -1071,6 +1071,7 @@ __global__ __launch_bounds__(kMaxBlock) void blob_chroma_meta_kernel(BlobArgs a,
         select2(w[i], d[i], cut[i], mm[i].x, mm[i].y, vm, e0, e1, q0, q1);
         cnt[i >> 1] += e0 + e1;  // one range: the spread masks are 0 or 1
         const uint64_t bal = q0 | q1;
+        if (bal == 0) continue;  // no lane of the wave flagged this word slot (the common case)
         const uint32_t idx =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
         if (__builtin_amdgcn_inverse_ballot_w64(bal)) {
