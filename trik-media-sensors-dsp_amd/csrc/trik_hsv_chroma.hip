@@ -788,9 +788,13 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
           return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         };
 #if TRIK_CHROMA_Q2
-        int total = 0;
+        // pre[i]: the step's flagged words before slot i (one scalar prefix
+        // chain gives the ranks' bases and the step total)
+        uint32_t pre[CW + 1];
+        pre[0] = 0;
 #pragma unroll
-        for (int i = 0; i < CW; ++i) total += __builtin_popcountll(bal[i]);
+        for (int i = 0; i < CW; ++i) pre[i + 1] = pre[i] + (uint32_t)__builtin_popcountll(bal[i]);
+        const int total = (int)pre[CW];
         // the whole step fits nearly always (qn < kDrainAt here, total ~15 of
         // at most 512): one basic block of EXEC-masked stores, no branch and
         // no drain check between the words; otherwise the queue is emptied
@@ -802,7 +806,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
           // entry index = the entries before this slot + the lane's rank (mbcnt
           // accumulates the scalar count; measured faster than a v_lshl_add on
           // an SGPR base, which waits for the SALU chain)
-          uint32_t at = (uint32_t)qn;
+          const uint32_t qtail = __builtin_amdgcn_readfirstlane(qbase_s + 8u * (uint32_t)qn);
 #pragma unroll
           for (int i = 0; i < CW; ++i) {
             // a slot no lane flagged skips its rank and store (one scalar
@@ -810,9 +814,8 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
             // -4 % on scene frames (profiles/r02h_skip_ab.txt)
             if (bal[i] == 0) continue;
             const uint32_t idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[i] >> 32),
-                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bal[i], at));
-            store_masked(bal[i], qbase_s + 8u * idx, cw[i], (i < 4 ? pos_s : pos_b) + xoff(i));
-            at += (uint32_t)__builtin_popcountll(bal[i]);
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bal[i], pre[i]));
+            store_masked(bal[i], qtail + 8u * idx, cw[i], (i < 4 ? pos_s : pos_b) + xoff(i));
           }
           qn += total;
         } else {
