@@ -114,3 +114,30 @@ def test_batches_hue_free(torch_dev, oracle_mod, name, w, h, layout, n, kind):
                 assert d.last_hot_kernel() == trik_hsv.HOT_STRIPE
         finally:
             d.close()
+
+
+@pytest.mark.parametrize("name,layout", [("v_bands", LAYOUT_YUYV), ("s_bands", LAYOUT_YUYV),
+                                         ("v_edge", LAYOUT_OV7670)])
+def test_padded_lines_hue_free(torch_dev, oracle_mod, name, layout):
+    """Padded lineLength and a frame stride that is not the frame size."""
+    import trik_hsv
+
+    torch = torch_dev
+    ranges = SETS[name]
+    w, h, n = 320, 64, 6
+    ll = (2 * w if layout == LAYOUT_YUYV else w) + 48
+    fb = trik_hsv.frame_bytes(w, h, ll, layout)
+    stride = fb + 64
+    host = oracle_mod.synth(n, w, h, ll, layout, 1, 0x9A7, first_frame=3)
+    padded = np.zeros(n * stride, np.uint8)
+    for i in range(n):
+        padded[i * stride:i * stride + fb] = host[i * fb:(i + 1) * fb]
+    want_s, want_t = oracle_mod.batch(host, fb, n, w, h, ll, layout, ranges, n_threads=8)
+    dev = torch.from_numpy(padded).cuda()
+    d = trik_hsv.Detector(hot=trik_hsv.HOT_STRIPE)
+    try:
+        sums, tg = d.process_batch(dev, w, h, ll, layout, ranges, n_frames=n, frame_stride=stride)
+        assert np.array_equal(sums.cpu().numpy(), want_s)
+        assert np.array_equal(tg[:, :, :3].cpu().numpy(), want_t)
+    finally:
+        d.close()
