@@ -488,8 +488,10 @@ int32_t trik_hsv_batch_sums(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvFra
  * picks the chroma-run kernel for batches of at least
  * TRIK_HSV_CHROMA_MIN_PIXELS pixels whose geometry it takes and whose range
  * set sends at most TRIK_HSV_CHROMA_MAX_SHARE of the words to its exact path
- * (see trik_hsv_chroma_share), the stripe kernel otherwise; the two give the
- * same results.  The first batch with a new range set is not held up by that
+ * (see trik_hsv_chroma_share), the stripe kernel otherwise -- always for a
+ * group of ranges that accepts every hue and saturation (value bands), which
+ * the stripe kernel tests by value alone; all kernels give the same results.
+ * The first batch with a new range set is not held up by that
  * share: both kernels are enqueued and the device runs the one the rule picks.
  * Returns the previous setting, or -1 for a NULL handle or an unknown kind. */
 #define TRIK_HSV_HOT_AUTO 0
