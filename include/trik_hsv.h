@@ -476,6 +476,18 @@ int32_t trik_hsv_process_batch(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsv
                                TrikHsvTargetSums* sums_dev, TrikHsvTarget* targets_dev,
                                void* hip_stream);
 
+/* The full batched step: as trik_hsv_process_batch, plus the per-target
+ * batch totals (totals_dev[r] = the sum over the frames of sums_dev[f][r], as
+ * trik_hsv_batch_totals).  Where the chroma-run kernel runs on a batch that
+ * gives every CU at least 4 whole frames, each group of <= 4 ranges is ONE
+ * launch: the kernel stores the sums (no zeroing), the targets and the totals
+ * itself; otherwise the same outputs come from the separate kernels.
+ * totals_dev: [n_ranges] TrikHsvTargetSums (device, not NULL). */
+int32_t trik_hsv_process_batch_totals(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvFrameBatch* batch,
+                                      const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int32_t n_ranges,
+                                      TrikHsvTargetSums* sums_dev, TrikHsvTarget* targets_dev,
+                                      TrikHsvTargetSums* totals_dev, void* hip_stream);
+
 /* Detect + reduce only; ADDS into sums_dev (caller zeroes it).  This is the
  * hot kernel, one launch per group of <= 4 ranges. */
 int32_t trik_hsv_batch_sums(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvFrameBatch* batch,
@@ -498,6 +510,7 @@ int32_t trik_hsv_batch_sums(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvFra
 #define TRIK_HSV_HOT_STRIPE 1
 #define TRIK_HSV_HOT_CHROMA 2
 #define TRIK_HSV_HOT_GENERIC 3
+#define TRIK_HSV_HOT_MIXED 4 /* trik_hsv_last_hot_kernel: the call's range groups ran different kernels */
 #define TRIK_HSV_CHROMA_MIN_PIXELS (32 * 640 * 480)
 #define TRIK_HSV_CHROMA_MAX_SHARE 0.25
 int32_t trik_hsv_set_hot_kernel(TRIK_VIDTRANSCODE_CV_Handle handle, int32_t kind);
@@ -506,8 +519,9 @@ int32_t trik_hsv_set_hot_kernel(TRIK_VIDTRANSCODE_CV_Handle handle, int32_t kind
  * 4 ranges), or -1 when its tables are not built.  Waits for the builder's
  * readback if it is still in flight.  Returns 0 or TRIK_IVIDTRANSCODE_EFAIL. */
 int32_t trik_hsv_chroma_share(TRIK_VIDTRANSCODE_CV_Handle handle, double* share);
-/* The kernel the handle's last hot launch ran (TRIK_HSV_HOT_STRIPE, _CHROMA or
- * _GENERIC; 0 before any).  When the device chose (see above) this waits for
+/* The kernel the handle's last hot call ran (TRIK_HSV_HOT_STRIPE, _CHROMA or
+ * _GENERIC; TRIK_HSV_HOT_MIXED when its groups of 4 ranges ran different
+ * kernels; 0 before any).  When the device chose (see above) this waits for
  * the builder's readback. */
 int32_t trik_hsv_last_hot_kernel(TRIK_VIDTRANSCODE_CV_Handle handle);
 

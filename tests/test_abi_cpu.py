@@ -130,3 +130,55 @@ def test_xdais_tables_link_from_c_and_alloc_without_gpu():
         r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
     assert len(r.stdout.split("\n")) >= 4
+
+
+XDAIS_FAIL_PROG = r"""
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "trik_hsv.h"
+/* TI's ALG_create after a failed algInit: algFree on the same record, which
+ * must find a valid object (destroyed once), then the record is released. */
+int main(void) {
+  const TRIK_IVIDTRANSCODE_Fxns* f = &TRIK_VIDTRANSCODE_CV_FXNS;
+  TRIK_IALG_MemRec m[4];
+  TRIK_IALG_Fxns* parent = NULL;
+  if (f->ialg.algAlloc(NULL, &parent, m) != 1) return 10;
+  void* rec = aligned_alloc(m[0].alignment < 16 ? 16 : m[0].alignment, (m[0].size + 63) / 64 * 64);
+  if (!rec) return 11;
+  memset(rec, 0xA5, m[0].size);
+  m[0].base = rec;
+  ((TRIK_IALG_Obj*)rec)->fxns = &f->ialg;
+  TRIK_VIDTRANSCODE_CV_Params p;
+  memset(&p, 0, sizeof p);
+  p.base.size = (int32_t)sizeof p;
+  p.base.numOutputStreams = 2;  /* WGLUE:96-101: rejected by setup */
+  /* fails on a machine without a HIP device (hipGetDevice) and on one with a
+   * device (the params): either way the object is left for algFree */
+  int rc = f->ialg.algInit((TRIK_IALG_Handle)rec, m, NULL, (const TRIK_IALG_Params*)&p);
+  if (rc == TRIK_IALG_EOK) return 12;
+  if (f->ialg.algFree((TRIK_IALG_Handle)rec, m) != 1 || m[0].base != rec) return 13;
+  free(rec);
+  printf("ok %d\n", rc);
+  return 0;
+}
+"""
+
+
+def build_xdais_fail(d):
+    lib_dir = os.path.join(ROOT, "trik-media-sensors-dsp_amd", "trik_hsv")
+    c, exe = os.path.join(d, "xf.c"), os.path.join(d, "xf")
+    open(c, "w").write(XDAIS_FAIL_PROG)
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", f"-I{os.path.join(ROOT, 'include')}", c,
+                    f"-L{lib_dir}", "-ltrik_hsv", f"-Wl,-rpath,{lib_dir}", "-o", exe], check=True)
+    return exe
+
+
+def test_xdais_algfree_after_failed_alginit():
+    """algInit fails (no HIP device here; rejected params on a GPU box):
+    algFree on the record then destroys the object once and returns the
+    record, as TI's ALG_create does after a failed algInit."""
+    with tempfile.TemporaryDirectory() as d:
+        r = subprocess.run([build_xdais_fail(d)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
+    assert r.stdout.startswith("ok")

@@ -255,11 +255,13 @@ struct TrikCvHandle {
   TableSet sets[kTableSets];
   uint64_t tick = 0;
   TableSet* sums_set = nullptr;  // the set of the last batched-sums call (trik_hsv_chroma_share)
-  // hot-kernel choice for this handle (trik_hsv_set_hot_kernel) and the kernel
-  // its last hot launch ran; pending_set: that launch let the device choose
-  // (the share was not known yet), resolved by trik_hsv_last_hot_kernel
+  // hot-kernel choice for this handle (trik_hsv_set_hot_kernel) and the
+  // kernel each range group of its last hot call ran (negative: the device
+  // chose between the chroma-run kernel and -kind by the group's cost, the
+  // share not being known yet; pending_set holds the costs), resolved by
+  // trik_hsv_last_hot_kernel
   std::atomic<int> hot{TRIK_HSV_HOT_AUTO};
-  int last_hot = 0;
+  std::vector<int8_t> hot_groups;
   TableSet* pending_set = nullptr;
 
   // preview geometry: scale maps for maps_key = {W, H, out_w, out_h}
@@ -280,6 +282,12 @@ struct TrikCvHandle {
   TrikHsvTargetSums* d_sums = nullptr;
   TrikHsvTarget* d_targets = nullptr;
 
+  // the chroma-run kernel's fused step: per-workgroup partial totals and the
+  // last-workgroup counter (0 between launches), shared by this handle's calls
+  unsigned long long* d_wg_part = nullptr;
+  uint32_t* d_wg_cnt = nullptr;
+  StreamUses fused_users;
+
   // ov7670 multi-blob sensor: BitmapBuilder's sticky range (uninitialised in
   // the reference before the first setHsvRange; zero here) and scratch
   TRIK_VIDTRANSCODE_CV_InArgsAlg blob_range{};  // as webcam-form bounds (all zero at first)
@@ -296,8 +304,9 @@ struct TrikCvHandle {
 
 namespace {
 
-void release(TrikCvHandle* h) {
-  if (!h) return;
+// The handle's device resources, freed; the object stays valid (null
+// pointers, no streams), so that this may run twice.
+void free_resources(TrikCvHandle* h) {
   int prev = 0;
   bool switched = hipGetDevice(&prev) == hipSuccess && prev != h->device &&
                   hipSetDevice(h->device) == hipSuccess;
@@ -307,6 +316,9 @@ void release(TrikCvHandle* h) {
   h->maps_users.release();
   h->blob_users.wait_all();
   h->blob_users.release();
+  h->fused_users.wait_all();
+  h->fused_users.release();
+  (void)hipFree(h->d_wg_part);
   (void)hipFree(h->d_frame);
   (void)hipFree(h->d_maps);
   (void)hipFree(h->d_preview);
@@ -319,6 +331,26 @@ void release(TrikCvHandle* h) {
   (void)hipFree(h->d_blob_targets);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   if (switched) (void)hipSetDevice(prev);
+  h->stream = nullptr;
+  h->d_frame = nullptr; h->d_frame_cap = 0;
+  h->d_maps = nullptr; h->d_maps_cap = 0;
+  h->maps_key[0] = -1;
+  h->d_preview = nullptr; h->d_preview_cap = 0;
+  h->d_auto = nullptr;
+  h->d_sums = nullptr;
+  h->d_targets = nullptr;
+  h->d_meta = nullptr; h->d_meta_cap = 0;
+  h->d_blob_stats = nullptr; h->d_blob_stats_cap = 0;
+  h->d_blob_top = nullptr; h->d_blob_top_cap = 0;
+  h->d_blob_targets = nullptr; h->d_blob_targets_cap = 0;
+  h->d_wg_part = nullptr; h->d_wg_cnt = nullptr;
+  h->sums_set = h->pending_set = nullptr;
+  h->alg_ready = false;
+}
+
+void release(TrikCvHandle* h) {
+  if (!h) return;
+  free_resources(h);
   if (h->owns_memory)
     delete h;
   else
@@ -417,6 +449,7 @@ int32_t acquire_tables(TrikCvHandle* h, const TRIK_VIDTRANSCODE_CV_InArgsAlg* ra
     if (v->ready) HIP_TRY(hipEventSynchronize(v->ready));
   }
   if (h->pending_set == v) h->pending_set = nullptr;
+  if (h->sums_set == v) h->sums_set = nullptr;
   const int groups = (n + kRangesPerLaunch - 1) / kRangesPerLaunch;
   if (groups > v->groups_cap) {
     v->release();
@@ -487,69 +520,137 @@ HotPlan plan_hot(TrikCvHandle* h, TableSet& t, int groups, bool big, bool chroma
   return sh <= TRIK_HSV_CHROMA_MAX_SHARE ? kPlanChroma : kPlanStripe;
 }
 
+// The outputs of a full step (process_batch): sums written whole (not added),
+// targets and the per-target batch totals when not NULL.
+struct StepOut {
+  TrikHsvTarget* targets = nullptr;
+  TrikHsvTargetSums* totals = nullptr;
+};
+
+// The fused step's scratch (one slot of 12 totals per CU, the counter zeroed
+// once), allocated on first use.
+int32_t ensure_fused_scratch(TrikCvHandle* h, hipStream_t s) {
+  if (h->d_wg_part) return 0;
+  const size_t parts = (size_t)device_cus() * 12;
+  void* p = nullptr;
+  HIP_TRY(hipMalloc(&p, sizeof(unsigned long long) * parts + 16));
+  h->d_wg_part = static_cast<unsigned long long*>(p);
+  h->d_wg_cnt = reinterpret_cast<uint32_t*>(h->d_wg_part + parts);
+  HIP_TRY(hipMemsetAsync(h->d_wg_cnt, 0, 16, s));
+  return 0;
+}
+
+// The hot kernel(s) over the batch: one launch per group of <= 4 ranges.
+// Without `step` the kernels ADD into sums (the caller zeroes it).  With it
+// the call is a full step: when every group runs the chroma-run kernel and the
+// batch gives each workgroup whole frames (chroma_fused_ok), each launch
+// stores its sums and writes its targets and totals itself (the fused step,
+// one launch per group); otherwise sums are zeroed first and the epilogue and
+// totals kernels follow.
 int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
                  const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, TrikHsvTargetSums* sums,
-                 uint8_t* masks, hipStream_t s) {
+                 uint8_t* masks, hipStream_t s, const StepOut* step = nullptr) {
   TableSet* t = nullptr;
   int32_t rc = acquire_tables(h, ranges, n, s, &t);
   if (rc) return rc;
   h->sums_set = t;
-  if (b->n_frames == 0 || b->width == 0 || b->height == 0) return 0;
+  const bool empty = b->n_frames == 0 || b->width == 0 || b->height == 0;
   const int groups = (n + kRangesPerLaunch - 1) / kRangesPerLaunch;
   const bool big = (int64_t)b->n_frames * b->width * b->height >= (int64_t)TRIK_HSV_CHROMA_MIN_PIXELS;
-  bool gated = false;
-  for (int g = 0; g < groups; ++g) {
-    KernelArgs a;
+  std::vector<KernelArgs> args(empty ? 0 : groups);
+  std::vector<HotPlan> plans(args.size(), kPlanStripe);
+  bool fused = step != nullptr && !masks && !empty;
+  for (size_t g = 0; g < args.size(); ++g) {
+    KernelArgs& a = args[g];
     a.frames = static_cast<const uint8_t*>(b->frames);
     a.frame_stride = b->n_frames > 1 ? b->frame_stride : 0;
     a.n_frames = b->n_frames;
     a.width = b->width; a.height = b->height; a.line_length = b->line_length;
     a.layout = b->layout;
-    a.n_ranges = n - g * kRangesPerLaunch < kRangesPerLaunch ? n - g * kRangesPerLaunch : kRangesPerLaunch;
-    a.range_offset = g * kRangesPerLaunch;
+    a.n_ranges = n - (int)g * kRangesPerLaunch < kRangesPerLaunch ? n - (int)g * kRangesPerLaunch : kRangesPerLaunch;
+    a.range_offset = (int)g * kRangesPerLaunch;
     a.sums_ranges = n;
     a.tables = t->d_tables + g;
     a.stripe_tables = t->d_stripe + g;
     a.detect_mode = t->detect[g];
     a.sums = sums;
     a.masks = masks;
-    a.mask_shift = g * kRangesPerLaunch;
+    a.mask_shift = (int)g * kRangesPerLaunch;
     // the chroma-run kernel for large batches, the stripe kernel otherwise;
     // the generic kernel takes misaligned inputs and rows wider than 8192 pixels
     // value-only groups (every range accepts every hue and saturation) run
     // the stripe kernel's value form under AUTO at any batch size: it beats
     // the chroma-run kernel there and needs no table build
-    const HotPlan plan = plan_hot(h, *t, groups, big && t->detect[g] != kDetectV,
-                                  h->hot.load() != TRIK_HSV_HOT_GENERIC && chroma_geometry_ok(a), s, &rc);
+    plans[g] = plan_hot(h, *t, groups, big && t->detect[g] != kDetectV,
+                        h->hot.load() != TRIK_HSV_HOT_GENERIC && chroma_geometry_ok(a), s, &rc);
     if (rc) return rc;
+    fused = fused && plans[g] == kPlanChroma && chroma_fused_ok(a);
+  }
+  if (fused) {
+    rc = ensure_fused_scratch(h, s);
+    if (rc) return rc;
+    HIP_TRY(h->fused_users.order_after(s));
+  }
+  if (step && !fused && !empty && sums)
+    HIP_TRY(hipMemsetAsync(sums, 0, sizeof(TrikHsvTargetSums) * (size_t)b->n_frames * n, s));
+  bool gated = false;
+  h->hot_groups.assign(groups, 0);
+  for (size_t g = 0; g < args.size(); ++g) {
+    KernelArgs& a = args[g];
+    const HotPlan plan = plans[g];
     int e = hipErrorNotSupported;
     if (plan == kPlanChroma) {
+      if (fused) {
+        a.fused = 1;
+        a.targets = step->targets;
+        a.totals = step->totals;
+        a.wg_part = h->d_wg_part;
+        a.wg_cnt = h->d_wg_cnt;
+      }
       e = launch_chroma(a, t->d_chroma + g, masks != nullptr, s);
-      if (e == hipSuccess) h->last_hot = TRIK_HSV_HOT_CHROMA;
+      if (e == hipSuccess) h->hot_groups[g] = TRIK_HSV_HOT_CHROMA;
     } else if (plan == kPlanGated) {
       // AUTO's rule on the device: the chroma-run kernel runs while this
-      // group's cost is at most kChromaMaxCost, the stripe kernel otherwise
+      // group's cost is at most kChromaMaxCost, its partner otherwise -- the
+      // stripe kernel, or the generic kernel where the stripe kernel's
+      // geometry does not take the batch (rows wider than 8192 pixels), with
+      // the same gate: exactly one of the two adds into the sums
       KernelArgs ac = a, as = a;
       ac.gate = as.gate = &t->d_chroma[g].flagged_cost;
       ac.gate_max = as.gate_max = kChromaMaxCost;
       ac.gate_le = 1;
       as.gate_le = 0;
       e = launch_chroma(ac, t->d_chroma + g, masks != nullptr, s);
-      if (e == hipSuccess) e = launch_stripe(as, masks != nullptr, s);
-      if (e == hipSuccess) gated = true;
+      if (e == hipSuccess) {
+        int partner = TRIK_HSV_HOT_STRIPE;
+        e = launch_stripe(as, masks != nullptr, s);
+        if (e == hipErrorNotSupported) {
+          partner = TRIK_HSV_HOT_GENERIC;
+          e = launch_reduce(as, masks != nullptr, s);
+        }
+        HIP_TRY(e);  // never an ungated launch after a gated one
+        h->hot_groups[g] = (int8_t)-partner;
+        gated = true;
+        continue;
+      }
     }
     if (e == hipErrorNotSupported && h->hot.load() != TRIK_HSV_HOT_GENERIC) {
       e = launch_stripe(a, masks != nullptr, s);
-      if (e == hipSuccess) h->last_hot = TRIK_HSV_HOT_STRIPE;
+      if (e == hipSuccess) h->hot_groups[g] = TRIK_HSV_HOT_STRIPE;
     }
     if (e == hipErrorNotSupported) {
       e = launch_reduce(a, masks != nullptr, s);
-      if (e == hipSuccess) h->last_hot = TRIK_HSV_HOT_GENERIC;
+      if (e == hipSuccess) h->hot_groups[g] = TRIK_HSV_HOT_GENERIC;
     }
     HIP_TRY(e);
   }
   h->pending_set = gated ? t : nullptr;
+  if (step && !fused) {  // the epilogue and the totals as kernels of their own
+    if (step->targets && !empty) HIP_TRY(launch_targets(*b, n, sums, step->targets, s));
+    if (step->totals) HIP_TRY(launch_totals(empty ? 0 : b->n_frames, n, sums, step->totals, s));
+  }
   rc = t->users.note(s);
+  if (!rc && fused) rc = h->fused_users.note(s);
   return rc ? fail(TRIK_IVIDTRANSCODE_EFAIL, std::string("hipEventRecord: ") + hipGetErrorString((hipError_t)rc)) : 0;
 }
 
@@ -753,10 +854,11 @@ int32_t run_blob(TrikCvHandle* h, BlobArgs& ba, TableSet& t, hipStream_t s) {
   if (rc) return rc;
   ba.meta_ready = 0;
   h->pending_set = nullptr;
+  h->hot_groups.assign(1, TRIK_HSV_HOT_STRIPE);
   if (plan == kPlanChroma) {
     HIP_TRY(launch_blob_meta_chroma(ba, t.d_chroma, t.d_tables, s));
     ba.meta_ready = 1;
-    h->last_hot = TRIK_HSV_HOT_CHROMA;
+    h->hot_groups[0] = TRIK_HSV_HOT_CHROMA;
   } else if (plan == kPlanGated) {  // both bitmap kernels, the device runs one (see run_sums)
     BlobArgs bc = ba;
     bc.gate = ba.gate = &t.d_chroma[0].flagged_cost;
@@ -765,8 +867,7 @@ int32_t run_blob(TrikCvHandle* h, BlobArgs& ba, TableSet& t, hipStream_t s) {
     ba.gate_le = 0;
     HIP_TRY(launch_blob_meta_chroma(bc, t.d_chroma, t.d_tables, s));
     h->pending_set = &t;
-  } else {
-    h->last_hot = TRIK_HSV_HOT_STRIPE;
+    h->hot_groups[0] = -TRIK_HSV_HOT_STRIPE;
   }
   HIP_TRY(launch_blob(ba, s));
   return 0;
@@ -802,11 +903,22 @@ static const TRIK_IALG_Fxns* table_of(int algo) {
   }
 }
 
+// A failed init: a handle of TRIK_VIDTRANSCODE_CV_create is deleted; one in
+// a framework record keeps a valid object without device resources, because
+// the framework calls algFree on it next (TI's ALG_create does), which
+// destroys it once.
+static void init_failed(TrikCvHandle* h) {
+  if (h->owns_memory)
+    release(h);
+  else
+    free_resources(h);
+}
+
 // trikCvHandleInit + SetupParams + SetupDynamicParams (WFXNS:146-166) on a
-// constructed object; releases it on failure.
+// constructed object; init_failed on failure.
 static int32_t init_handle(TrikCvHandle* h, int algo, const TRIK_VIDTRANSCODE_CV_Params* params) {
   if (hipGetDevice(&h->device) != hipSuccess) {
-    release(h);
+    init_failed(h);
     return fail(TRIK_IALG_EFAIL, "no HIP device");
   }
   h->algo = algo;
@@ -816,7 +928,7 @@ static int32_t init_handle(TrikCvHandle* h, int algo, const TRIK_VIDTRANSCODE_CV
   // (the webcam line sensor's glue has the webcam object sensor's Params)
   const int32_t rc = setup_dynamic(h, nullptr);      // WFXNS:158-163
   if (rc != TRIK_IALG_EOK) {
-    release(h);
+    init_failed(h);
     return rc;
   }
   return TRIK_IALG_EOK;
@@ -1309,14 +1421,23 @@ extern "C" int32_t trik_hsv_set_hot_kernel(TRIK_VIDTRANSCODE_CV_Handle h, int32_
 extern "C" int32_t trik_hsv_last_hot_kernel(TRIK_VIDTRANSCODE_CV_Handle h) {
   if (!h) return 0;
   std::lock_guard<std::mutex> lock(h->mu);
-  if (h->pending_set) {  // the device chose: resolve it from the builder's cost
+  if (h->pending_set) {  // the device chose: resolve each gated group from its builder cost
     DeviceGuard dg(h->device);
     TableSet* t = h->pending_set;
     (void)hipEventSynchronize(t->cost_ready);
-    h->last_hot = t->share() <= TRIK_HSV_CHROMA_MAX_SHARE ? TRIK_HSV_HOT_CHROMA : TRIK_HSV_HOT_STRIPE;
+    for (size_t g = 0; g < h->hot_groups.size(); ++g)
+      if (h->hot_groups[g] < 0)
+        h->hot_groups[g] = (int8_t)(g < (size_t)t->groups_cap && t->h_cost[g] <= kChromaMaxCost
+                                        ? TRIK_HSV_HOT_CHROMA
+                                        : -h->hot_groups[g]);
     h->pending_set = nullptr;
   }
-  return h->last_hot;
+  int kind = 0;
+  for (int8_t k : h->hot_groups) {
+    if (!k) continue;
+    kind = kind == 0 || kind == k ? k : TRIK_HSV_HOT_MIXED;
+  }
+  return kind;
 }
 
 extern "C" int32_t trik_hsv_chroma_share(TRIK_VIDTRANSCODE_CV_Handle h, double* share) {
@@ -1398,12 +1519,27 @@ extern "C" int32_t trik_hsv_process_batch(TRIK_VIDTRANSCODE_CV_Handle h, const T
   hipStream_t s = static_cast<hipStream_t>(stream);
   std::lock_guard<std::mutex> lock(h->mu);
   DeviceGuard dg(h->device);
-  if (b->n_frames > 0)
-    HIP_TRY(hipMemsetAsync(sums, 0, sizeof(TrikHsvTargetSums) * (size_t)b->n_frames * n, s));
-  rc = run_sums(h, b, ranges, n, sums, nullptr, s);
+  StepOut step;
+  step.targets = targets;
+  return run_sums(h, b, ranges, n, sums, nullptr, s, &step);
+}
+
+extern "C" int32_t trik_hsv_process_batch_totals(TRIK_VIDTRANSCODE_CV_Handle h, const TrikHsvFrameBatch* b,
+                                                 const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int32_t n,
+                                                 TrikHsvTargetSums* sums, TrikHsvTarget* targets,
+                                                 TrikHsvTargetSums* totals, void* stream) {
+  int32_t rc = check_common(h, b, ranges, n, sums);
   if (rc) return rc;
-  if (targets) HIP_TRY(launch_targets(*b, n, sums, targets, s));
-  return 0;
+  if (!totals) return fail(TRIK_IVIDTRANSCODE_EFAIL, "totals is NULL");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  std::lock_guard<std::mutex> lock(h->mu);
+  DeviceGuard dg(h->device);
+  rc = check_device(h, b, totals);
+  if (rc) return rc;
+  StepOut step;
+  step.targets = targets;
+  step.totals = totals;
+  return run_sums(h, b, ranges, n, sums, nullptr, s, &step);
 }
 
 extern "C" int32_t trik_hsv_batch_masks(TRIK_VIDTRANSCODE_CV_Handle h, const TrikHsvFrameBatch* b,

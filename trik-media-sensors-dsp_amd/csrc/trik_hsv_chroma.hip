@@ -45,36 +45,20 @@ namespace trik_hsv {
 namespace {
 
 constexpr int kMaxBlock = 1024;
-#ifndef TRIK_CHROMA_NT
-#define TRIK_CHROMA_NT 1  // YUYV frame loads with the nontemporal hint
-#endif
-#ifndef TRIK_CHROMA_SPLITB
-#define TRIK_CHROMA_SPLITB 0  // block words as two byte tables (pair offset, cut): -3 VALU per word, but one more LDS read; measured slower
-#endif
-#ifndef TRIK_CHROMA_Q2
-#define TRIK_CHROMA_Q2 1  // queue appends batched per step, EXEC-masked stores without branches
-#endif
-#ifndef TRIK_CHROMA_CW
-#define TRIK_CHROMA_CW 8
-#endif
-constexpr int kChunkWords = TRIK_CHROMA_CW;  // YUYV words per lane and row (8: 32 bytes, 16 pixels)
-static_assert(kChunkWords == 4 || kChunkWords == 8, "chunk width");
+constexpr int kChunkWords = 8;  // YUYV words per lane and step (two 4-word pieces, 16 pixels)
 // steps per tile: byte counters P_i <= 2 * steps, O <= kChunkWords * steps
-constexpr int kMaxSteps = kChunkWords == 8 ? 31 : 63;
-static_assert((kChunkWords == 8 ? 4 : 2) * 2 * kMaxSteps <= 255, "flush group sums fit a byte");
-constexpr int kQFlush = 7;
+constexpr int kMaxSteps = 31;
+static_assert(4 * 2 * kMaxSteps <= 255, "flush group sums fit a byte");
 constexpr int kQueueCap = 128;  // blob kernel, entries per wave: < 64 waiting + <= 64 added by one word slot
-// Hot kernel: at most 15 waves (960 lanes) per workgroup; a wave drains its
-// queue down to < kDrainAt entries after every step, and a step appends its
-// words at once when they fit (else word by word, draining before each).
+// Hot kernel: at most 15 waves (960 lanes) per workgroup.  A lane's step is
+// two pieces of 4 words; a piece with a flagged word becomes one record of
+// the wave's queue (its 4 words + a meta word), so a step costs two
+// compactions, not one per word slot.  kRecCap records per wave is what the
+// LDS image leaves; a step starts with < 64 records queued.
 constexpr int kHotLanes = 960;
-constexpr int kHotQueueCap = 53 + 128;  // what the LDS image leaves: 15 x 181 x 8 B (+ 15 x 48 B of rare sums)
-// per-step appends drain full rounds of 64; word-by-word appends (A/B) drain at
-// 60 every second word, so the queue holds < 60 + 128 entries
-#ifndef TRIK_CHROMA_DRAIN_AT
-#define TRIK_CHROMA_DRAIN_AT 64
-#endif
-constexpr int kDrainAt = TRIK_CHROMA_Q2 ? TRIK_CHROMA_DRAIN_AT : 60;
+constexpr int kRecCap = 73;
+// fused step: frames in flight per workgroup (a ring of LDS accumulators)
+constexpr int kFrameSlots = 4;
 
 // LDS image of the chroma kernel (dynamic LDS from address 0).  The block
 // masks and the mask-pair table sit below 64 KiB so their reads take an
@@ -87,20 +71,21 @@ constexpr uint32_t kLdsHue = kLdsLut255 + 512;        // u8  [256]   hue test pe
 constexpr uint32_t kLdsSat = kLdsHue + 256;           // u8  [256]   saturation test per S
 constexpr uint32_t kLdsVal = kLdsSat + 256;           // u8  [256]   value test per V
 constexpr uint32_t kLdsRuns = kLdsVal + 256;          // u16 [65536] b1 | b2 << 8 per chroma
-constexpr uint32_t kLdsQueues = kLdsRuns + 131072;    // per wave: kHotQueueCap (blob: kQueueCap) x {word, pos}
+constexpr uint32_t kLdsQueues = kLdsRuns + 131072;    // blob kernel: per wave kQueueCap x {word, pos}
 static_assert(kLdsBlocks + 8192 <= kLdsPairs, "LDS layout");
-// The hot kernel keeps the block words as two byte tables in the same 8 KiB:
-// the pair's palette offset and the cut, both indexed by the block c >> 4
-// (one shift for both addresses; the offset byte is the pair's address).
-#if TRIK_CHROMA_SPLITB
-constexpr uint32_t kLdsBlkPair = kLdsBlocks;          // u8 [4096]
-constexpr uint32_t kLdsBlkCut = kLdsBlocks + 4096;    // u8 [4096]
-#endif
-// per wave: the 12 u32 sums (3 per range) of the words the rare overflow
-// path resolved (drain_rare), added to the wave's sums at the tile end
-constexpr uint32_t kLdsRare = kLdsQueues + (kHotLanes / 64) * kHotQueueCap * 8;
-constexpr uint32_t kLdsBytes = kLdsRare + (kHotLanes / 64) * 48;
+// hot kernel records: per wave kRecCap x 16 B of words, then all waves' meta
+// words (kRecCap x 4 B per wave): f (bits 0-3: the piece's flagged words) |
+// x / 8 (bits 4-15) | row in the tile (bits 16-31)
+constexpr uint32_t kLdsRecWords = kLdsQueues;
+constexpr uint32_t kLdsRecMeta = kLdsRecWords + (kHotLanes / 64) * kRecCap * 16;
+// fused step: per frame slot 12 u64 sums (3 per range), the waves' arrival
+// count and the frame the slot takes (tag); then the workgroup's 12 u64 totals
+constexpr uint32_t kFrameSlotBytes = 12 * 8 + 8;
+constexpr uint32_t kLdsFrames = (kLdsRecMeta + (kHotLanes / 64) * kRecCap * 4 + 7u) & ~7u;
+constexpr uint32_t kLdsTotals = kLdsFrames + kFrameSlots * kFrameSlotBytes;
+constexpr uint32_t kLdsBytes = kLdsTotals + 12 * 8 + 8;  // + the last-workgroup flag
 static_assert(kLdsBytes <= 160 * 1024, "chroma kernel LDS image");
+static_assert((kRecCap * 16) % 16 == 0 && kRecCap >= 64 + 8, "record queue");
 
 typedef __attribute__((address_space(3))) uint8_t* lds8_t;
 typedef __attribute__((address_space(3))) uint16_t* lds16_t;
@@ -112,6 +97,32 @@ typedef __attribute__((address_space(3))) u32x4* lds128_t;
 __device__ __forceinline__ uint32_t ld8(uint32_t a) { return *(lds8_t)(uintptr_t)a; }
 __device__ __forceinline__ uint32_t ld16(uint32_t a) { return *(lds16_t)(uintptr_t)a; }
 __device__ __forceinline__ u32x2 ld64(uint32_t a) { return *(lds64_t)(uintptr_t)a; }
+__device__ __forceinline__ unsigned long long ld_u64(uint32_t a) {
+  return *(__attribute__((address_space(3))) unsigned long long*)(uintptr_t)a;
+}
+__device__ __forceinline__ void st_u64(uint32_t a, unsigned long long v) {
+  *(__attribute__((address_space(3))) unsigned long long*)(uintptr_t)a = v;
+}
+// the fused step's frame-slot tags: acquire loads, release stores (the slot's
+// sums are zeroed before its tag moves on)
+__device__ __forceinline__ uint32_t ld_acquire(uint32_t a) {
+  return __hip_atomic_load((__attribute__((address_space(3))) uint32_t*)(uintptr_t)a, __ATOMIC_ACQUIRE,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void st_release(uint32_t a, uint32_t v) {
+  __hip_atomic_store((__attribute__((address_space(3))) uint32_t*)(uintptr_t)a, v, __ATOMIC_RELEASE,
+                     __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_add_u64(uint32_t a, unsigned long long v) {
+  __hip_atomic_fetch_add((__attribute__((address_space(3))) unsigned long long*)(uintptr_t)a, v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// a frame slot's arrival count: acq_rel, so a wave's sums are added before it
+// counts itself and the last wave reads them after
+__device__ __forceinline__ uint32_t lds_add_rtn_u32(uint32_t a, uint32_t v) {
+  return __hip_atomic_fetch_add((__attribute__((address_space(3))) uint32_t*)(uintptr_t)a, v, __ATOMIC_ACQ_REL,
+                                __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 __device__ __forceinline__ void st64(uint32_t a, uint32_t x, uint32_t y) {
   u32x2 v;
   v.x = x;
@@ -164,19 +175,26 @@ __device__ __forceinline__ void select2(uint32_t w, uint32_t d, uint32_t bw, uin
       : [m1] "v"(m1), [m2] "v"(m2), [lt0] "s"(lt0), [lt1] "s"(lt1), [k0] "s"(k0), [k1] "s"(k1));
 }
 
-// Queue store of (w, pos) at LDS address qa by the lanes of wave mask m only:
-// EXEC narrowed and restored inside one asm block (no branch, so the stores
-// of a step's words stay in one basic block).  The compiler's own LDS
-// counters stay conservative: LDS operations of a wave complete in order.
-__device__ __forceinline__ void store_masked(uint64_t m, uint32_t qa, uint32_t w, uint32_t pos) {
+// Record store (a piece's 4 words at wa, its meta word at ma) by the lanes of
+// wave mask m only: EXEC narrowed and restored inside one asm block (no
+// branch).  The compiler's own LDS counters stay conservative: LDS operations
+// of a wave complete in order.
+__device__ __forceinline__ void store_record(uint64_t m, uint32_t wa, u32x4 w, uint32_t ma, uint32_t meta) {
   uint64_t saved;
   asm volatile(
       "s_and_saveexec_b64 %[sv], %[m]\n\t"
-      "ds_write2_b32 %[a], %[w], %[p] offset1:1\n\t"
+      "ds_write_b128 %[wa], %[w]\n\t"
+      "ds_write_b32 %[ma], %[mt]\n\t"
       "s_mov_b64 exec, %[sv]"
       : [sv] "=&s"(saved)
-      : [m] "s"(m), [a] "v"(qa), [w] "v"(w), [p] "v"(pos)
+      : [m] "s"(m), [wa] "v"(wa), [w] "v"(w), [ma] "v"(ma), [mt] "v"(meta)
       : "memory", "scc");
+}
+
+// v if this lane's bit of wave mask m is set, else 0 (one v_cndmask; a
+// v_addc shift-in chain needs a wait state after every op on gfx950)
+__device__ __forceinline__ uint32_t lane_bit(uint64_t m, uint32_t v) {
+  return __builtin_amdgcn_inverse_ballot_w64(m) ? v : 0u;
 }
 
 // 4-bit mask (range t -> bit t) -> byte-spread (range t -> bit 8t)
@@ -461,39 +479,24 @@ __device__ __forceinline__ void wave_sums12(uint32_t (&v)[12]) {
   for (int i = 0; i < 3; ++i) v[i] += __builtin_amdgcn_update_dpp(0u, v[i], 0x118, 0xF, 0xF, true);
 }
 
-// One chunk = CW YUYV words (2*CW pixels): YUYV, two 16-byte pieces (8
-// pixels each) at p and pb -- the same columns of two rows, so that one load
-// instruction of a wave reads 1 KiB contiguous; ov7670, 2*CW luma + 2*CW
-// chroma bytes of one row of the two planes (pb unused).
-template <int LAYOUT, int CW>
-__device__ __forceinline__ void load_chunk(const uint8_t* p, const uint8_t* pb, int64_t plane,
-                                           uint32_t (&w)[CW]) {
+// One chunk = 8 YUYV words (16 pixels) in two 4-word pieces: YUYV, two
+// 16-byte pieces (8 pixels each) at p and pb -- the same columns of two rows,
+// so that one load instruction of a wave reads 1 KiB contiguous; ov7670, 16
+// luma + 16 chroma bytes of one row of the two planes (pb unused).
+template <int LAYOUT>
+__device__ __forceinline__ void load_chunk(const uint8_t* p, const uint8_t* pb, int64_t plane, uint32_t (&w)[8]) {
   if (LAYOUT == TRIK_HSV_LAYOUT_YUYV) {
-    static_assert(CW == 8, "YUYV chunks are two 16-byte pieces");
-#if TRIK_CHROMA_NT
     const u32x4 va = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
     const u32x4 vb = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pb));
-#else
-    const uint4 va = *reinterpret_cast<const uint4*>(p), vb = *reinterpret_cast<const uint4*>(pb);
-#endif
     w[0] = va.x; w[1] = va.y; w[2] = va.z; w[3] = va.w;
     w[4] = vb.x; w[5] = vb.y; w[6] = vb.z; w[7] = vb.w;
   } else {
-    uint32_t yy[CW / 2], cc[CW / 2];
-    if (CW == 8) {
-      const uint4 vy = *reinterpret_cast<const uint4*>(p);
-      const uint4 vc = *reinterpret_cast<const uint4*>(p + plane);
-      yy[0] = vy.x; yy[1] = vy.y; yy[CW / 2 - 2] = vy.z; yy[CW / 2 - 1] = vy.w;
-      cc[0] = vc.x; cc[1] = vc.y; cc[CW / 2 - 2] = vc.z; cc[CW / 2 - 1] = vc.w;
-    } else {
-      const uint2 vy = *reinterpret_cast<const uint2*>(p);
-      const uint2 vc = *reinterpret_cast<const uint2*>(p + plane);
-      yy[0] = vy.x; yy[CW / 2 - 1] = vy.y;
-      cc[0] = vc.x; cc[CW / 2 - 1] = vc.y;
-    }
+    const uint4 vy = *reinterpret_cast<const uint4*>(p);
+    const uint4 vc = *reinterpret_cast<const uint4*>(p + plane);
+    const uint32_t yy[4] = {vy.x, vy.y, vy.z, vy.w}, cc[4] = {vc.x, vc.y, vc.z, vc.w};
     // OSEQ:369-373: U = odd chroma byte, V = even chroma byte
 #pragma unroll
-    for (int j = 0; j < CW / 2; ++j) {
+    for (int j = 0; j < 4; ++j) {
       w[2 * j] = __builtin_amdgcn_perm(cc[j], yy[j], 0x04010500u);
       w[2 * j + 1] = __builtin_amdgcn_perm(cc[j], yy[j], 0x06030702u);
     }
@@ -535,25 +538,17 @@ struct ExcSums {
   int rounds = 0;
 };
 
-template <int LAYOUT, int NR, bool MASKS, int CW>
+template <int LAYOUT, int NR, bool MASKS>
 __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaGeom g, const ChromaTables* ct) {
   if (gated_out(a.gate, a.gate_max, a.gate_le)) return;
+  constexpr int CW = kChunkWords;
   const int t = threadIdx.x;
-  {  // stage the block bytes, the mask-pair table and the run descriptors
-#if TRIK_CHROMA_SPLITB
-    for (int i = t; i < 4096 / 4; i += blockDim.x) {  // 4 block words -> 4 pair bytes + 4 cut bytes
-      const u32x2 bw = reinterpret_cast<const u32x2*>(ct->blocks)[i];
-      *(lds32_t)(uintptr_t)(kLdsBlkPair + 4 * i) = __builtin_amdgcn_perm(bw.y, bw.x, 0x06040200u);
-      *(lds32_t)(uintptr_t)(kLdsBlkCut + 4 * i) = __builtin_amdgcn_perm(bw.y, bw.x, 0x07050301u);
-    }
-#else
+  {  // stage the block words, the mask-pair table, the run descriptors and the exact-path tables
     for (int i = t; i < 8192 / 16; i += blockDim.x)
       *(lds128_t)(uintptr_t)(kLdsBlocks + 16 * i) = reinterpret_cast<const u32x4*>(ct->blocks)[i];
-#endif
     for (int i = t; i < kChromaPalette; i += blockDim.x) st64(kLdsPairs + 8 * i, ct->palette[2 * i], ct->palette[2 * i + 1]);
     for (int i = t; i < 131072 / 16; i += blockDim.x)
       *(lds128_t)(uintptr_t)(kLdsRuns + 16 * i) = reinterpret_cast<const u32x4*>(ct->runs)[i];
-    for (int i = t; i < (kHotLanes / 64) * 12; i += blockDim.x) *(lds32_t)(uintptr_t)(kLdsRare + 4 * i) = 0u;
     for (int i = t; i < 256; i += blockDim.x) {
       *(lds16_t)(uintptr_t)(kLdsLut43 + 2 * i) = a.tables->lut43[i];
       *(lds16_t)(uintptr_t)(kLdsLut255 + 2 * i) = a.tables->lut255[i];
@@ -562,30 +557,48 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
       *(lds8_t)(uintptr_t)(kLdsVal + i) = a.tables->vmask[i];
     }
   }
+  // fused step: this workgroup's frames [f_first, f_end) (whole frames), its
+  // tiles; the frame slots' sums zeroed and tagged with their first frames
+  const int64_t f_first = a.fused ? (int64_t)a.n_frames * blockIdx.x / gridDim.x : 0;
+  const int64_t t_begin = a.fused ? f_first * g.tiles_per_frame : g.n_tiles * blockIdx.x / gridDim.x;
+  const int64_t t_end = a.fused ? (int64_t)a.n_frames * (blockIdx.x + 1) / gridDim.x * g.tiles_per_frame
+                                : g.n_tiles * (blockIdx.x + 1) / gridDim.x;
+  if (a.fused) {
+    if (t < kFrameSlots * 12) st_u64(kLdsFrames + (t / 12) * kFrameSlotBytes + 8 * (t % 12), 0ull);
+    if (t < kFrameSlots) {
+      *(lds32_t)(uintptr_t)(kLdsFrames + t * kFrameSlotBytes + 96) = 0u;
+      *(lds32_t)(uintptr_t)(kLdsFrames + t * kFrameSlotBytes + 100) = (uint32_t)(f_first + t);
+    }
+    if (t < 12) st_u64(kLdsTotals + 8 * t, 0ull);
+  }
   __syncthreads();
 
   const int lane = t & 63;
-  const uint32_t qbase_s = __builtin_amdgcn_readfirstlane(kLdsQueues + (uint32_t)(t >> 6) * (kHotQueueCap * 8));
-  const uint32_t rare_s = __builtin_amdgcn_readfirstlane(kLdsRare + (uint32_t)(t >> 6) * 48u);
+  const uint32_t wave = (uint32_t)(t >> 6);
+  const uint32_t rw_s = __builtin_amdgcn_readfirstlane(kLdsRecWords + wave * (kRecCap * 16u));
+  const uint32_t rm_s = __builtin_amdgcn_readfirstlane(kLdsRecMeta + wave * (kRecCap * 4u));
   const bool active = t < g.k * g.cpr;
   const int col = active ? t % g.cpr : 0;
   const int ro = active ? t / g.cpr : 0;
-  // YUYV: a lane's 8 words are 4 from row y and 4 from row y + k (word i at
-  // x0 + 2 (i & 3)); ov7670: 8 words of row y (word i at x0 + 2i)
+  // YUYV: a lane's 8 words are 4 from row y (piece a) and 4 from row y + dy,
+  // dx pixels right (piece b; word i at x0 + 2 (i & 3)); ov7670: 8 words of
+  // row y (piece b 8 pixels right; word i at x0 + 2i)
   constexpr bool SPLIT = LAYOUT == TRIK_HSV_LAYOUT_YUYV;
   const int64_t plane = (int64_t)a.height * a.line_length;
   const int64_t rowstep = (int64_t)g.rstep * a.line_length;
   const int half = SPLIT ? g.dy : 0;  // rows between a chunk's two pieces
   const uint32_t dx = SPLIT ? (uint32_t)g.dx : 0u;  // and pixels
   const int64_t hb = (int64_t)half * a.line_length + 2 * (int64_t)dx;
-  constexpr int kQBlock = CW == 8 ? 5 : kQFlush;  // Q block: CW * n * (n + 1) <= 255
+  constexpr int kQBlock = 5;  // Q block: CW * n * (n + 1) <= 255
   const int col_bytes = LAYOUT == TRIK_HSV_LAYOUT_YUYV ? col * 16 : col * 2 * CW;
   const uint32_t x0 = (uint32_t)col * (SPLIT ? 8u : 2u * CW);
   const uint32_t voff = (uint32_t)ro * (uint32_t)a.line_length + (uint32_t)col_bytes;
   auto xoff = [=](int i) { return SPLIT ? (i < 4 ? 0u : dx) + 2u * (uint32_t)(i & 3) : 2u * (uint32_t)i; };
+  // a record's meta word without its flag bits: x / 8 of the piece's first
+  // pixel and its row in the tile (piece b: xb8 * 8 pixels right, half rows down)
+  const uint32_t meta_x = (x0 >> 3) << 4;
+  const uint32_t meta_b = ((SPLIT ? dx >> 3 : 1u) << 4) + ((uint32_t)half << 16);
 
-  const int64_t t_begin = g.n_tiles * blockIdx.x / gridDim.x;
-  const int64_t t_end = g.n_tiles * (blockIdx.x + 1) / gridDim.x;
   // the frame and the tile within it, stepped along (wave-uniform, SALU)
   int fcur = __builtin_amdgcn_readfirstlane((int)(t_begin / g.tiles_per_frame));
   int trem = __builtin_amdgcn_readfirstlane((int)(t_begin - (int64_t)fcur * g.tiles_per_frame));
@@ -605,7 +618,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     for (int i = 0; i < CW; ++i) P[i] = 0;
     uint32_t Qa = 0, Qb = 0, Ba = 0, Bb = 0;
     int nb = 0;
-    // exception queue (wave-uniform count) and this lane's exception sums
+    // record queue (wave-uniform count) and this lane's exact-path sums
     int qn = 0;
     ExcSums ex;
     uint32_t xacc[3 * NR];
@@ -625,32 +638,37 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
       ex.EN = ex.SX02 = ex.SX13 = ex.SY02 = ex.SY13 = 0;
       ex.rounds = 0;
     };
-    // One drain round: lanes 0..take-1 resolve the last take queue entries
-    // (two pixels each) exactly.
-    // The exact masks of the flagged pixels of queue entry qn - take + lane
-    // (which of the word's pixels the fast path left to this path: select2);
-    // verification mode writes them.
-    auto resolve = [&](int take, uint32_t& x, uint32_t& yr, uint32_t& m0, uint32_t& m1) {
-      const u32x2 ent = ld64(qbase_s + 8u * (uint32_t)(qn - take + lane));
-      const uint32_t w = ent.x;
-      x = ent.y & 0xFFFFu;
-      yr = ent.y >> 16;
-      const uint32_t d = ld16(kLdsRuns + 2u * chroma_of(w));
-      const uint32_t lo = d & 0xFFu, hi = d >> 8, Y0 = w & 0xFFu, Y1 = (w >> 16) & 0xFFu;
-      const bool xw = d == kChromaExc;
-      const bool f0 = xw | ((Y0 < lo) & (Y0 > hi)), f1 = xw | ((Y1 < lo) & (Y1 > hi));
-      m0 = f0 ? exact_mask<0>(w) : 0u;
-      m1 = f1 ? exact_mask<1>(w) : 0u;
-      if (MASKS) {
-        uint8_t* mp = a.masks + ((int64_t)f * a.height + r0 + yr) * a.width + x;
-        if (f0) mp[0] = a.mask_shift ? (uint8_t)(mp[0] | (m0 << a.mask_shift)) : (uint8_t)m0;
-        if (f1) mp[1] = a.mask_shift ? (uint8_t)(mp[1] | (m1 << a.mask_shift)) : (uint8_t)m1;
-      }
-    };
+    // One drain round: lanes 0..take-1 take the last take records, resolve
+    // the first flagged word of each exactly (which of its pixels the fast
+    // path left to this path: select2; the exact masks: exact_mask) and
+    // accumulate them with explicit (x, y); a record with more flagged words
+    // goes back to the queue with its remaining bits.  Verification mode
+    // writes the exact masks.
     auto drain = [&](int take) {
-      if (lane < take) {
-        uint32_t x, yr, m0, m1;
-        resolve(take, x, yr, m0, m1);
+      const uint32_t base = (uint32_t)(qn - take);
+      const bool act = lane < take;
+      u32x4 w4 = {0u, 0u, 0u, 0u};
+      uint32_t meta = 0;
+      if (act) {
+        w4 = *(lds128_t)(uintptr_t)(rw_s + 16u * (base + (uint32_t)lane));
+        meta = *(lds32_t)(uintptr_t)(rm_s + 4u * (base + (uint32_t)lane));
+      }
+      const uint32_t fl = meta & 15u;
+      if (act) {
+        const uint32_t i = (uint32_t)__builtin_ctz(fl);
+        const uint32_t w = (i & 2u) ? ((i & 1u) ? w4.w : w4.z) : ((i & 1u) ? w4.y : w4.x);
+        const uint32_t x = ((meta >> 4) & 0xFFFu) * 8u + 2u * i, yr = meta >> 16;
+        const uint32_t d = ld16(kLdsRuns + 2u * chroma_of(w));
+        const uint32_t lo = d & 0xFFu, hi = d >> 8, Y0 = w & 0xFFu, Y1 = (w >> 16) & 0xFFu;
+        const bool xw = d == kChromaExc;
+        const bool f0 = xw | ((Y0 < lo) & (Y0 > hi)), f1 = xw | ((Y1 < lo) & (Y1 > hi));
+        const uint32_t m0 = f0 ? exact_mask<0>(w) : 0u;
+        const uint32_t m1 = f1 ? exact_mask<1>(w) : 0u;
+        if (MASKS) {
+          uint8_t* mp = a.masks + ((int64_t)f * a.height + r0 + yr) * a.width + x;
+          if (f0) mp[0] = a.mask_shift ? (uint8_t)(mp[0] | (m0 << a.mask_shift)) : (uint8_t)m0;
+          if (f1) mp[1] = a.mask_shift ? (uint8_t)(mp[1] | (m1 << a.mask_shift)) : (uint8_t)m1;
+        }
         const uint32_t e0 = spread4(m0), e1 = spread4(m1);
         ex.EN += e0 + e1;
         const uint32_t a0 = e0 & 0x00FF00FFu, a1 = e1 & 0x00FF00FFu;
@@ -661,39 +679,29 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         ex.SY13 += (b0 + b1) * yr;
       }
       if (++ex.rounds == g.flush_rounds) unpack_exc();
-      __builtin_amdgcn_wave_barrier();  // the entries are read before the slots are reused
-      qn -= take;
-    };
-    // The same round for the rare overflow cases (a step whose words do not
-    // fit the queue): its sums go to the wave's LDS slots, not to the lane
-    // registers, so that the per-step path carries no second version of the
-    // lane sums (a register-merge copy of 17 values per step otherwise).
-    auto drain_rare = [&](int take) {
-      uint32_t v[12];
-#pragma unroll
-      for (int i = 0; i < 12; ++i) v[i] = 0u;
-      if (lane < take) {
-        uint32_t x, yr, m0, m1;
-        resolve(take, x, yr, m0, m1);
-        const uint32_t y = (uint32_t)r0 + yr;
-#pragma unroll
-        for (int rr = 0; rr < NR; ++rr) {
-          const uint32_t b0 = (m0 >> rr) & 1u, b1 = (m1 >> rr) & 1u;
-          v[3 * rr] = b0 + b1;
-          v[3 * rr + 1] = (b0 + b1) * x + b1;
-          v[3 * rr + 2] = (b0 + b1) * y;
-        }
-      }
-      wave_sums12(v);
-      if ((lane & 15) == 15 && (lane >> 4) < NR) {
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {  // one lane per slot: no atomics
-          const uint32_t ra = rare_s + 12u * (uint32_t)(lane >> 4) + 4u * i;
-          *(lds32_t)(uintptr_t)ra = *(lds32_t)(uintptr_t)ra + v[i];
-        }
+      // records with flagged words left go back, compacted, where the
+      // drained ones were (their reads above come first: LDS is in order)
+      const uint32_t rest = fl & (fl - 1u);
+      const uint64_t left = __builtin_amdgcn_ballot_w64(rest != 0u);
+      if (left) {
+        const uint32_t idx =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(left >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)left, base));
+        store_record(left, rw_s + 16u * idx, w4, rm_s + 4u * idx, (meta & ~15u) | rest);
       }
       __builtin_amdgcn_wave_barrier();
-      qn -= take;
+      qn = (int)base + (int)__builtin_popcountll(left);
+    };
+    // Append the records of one piece slot (wave mask m: the lanes whose
+    // piece has a flagged word; meta with their flag bits), draining first
+    // when the queue cannot take them.
+    auto append = [&](uint64_t m, u32x4 w4, uint32_t meta) {
+      if (m == 0) return;
+      const int cnt = (int)__builtin_popcountll(m);
+      while (qn + cnt > kRecCap) drain(qn < 64 ? qn : 64);
+      const uint32_t idx =
+          __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)qn));
+      store_record(m, rw_s + 16u * idx, w4, rm_s + 4u * idx, meta);
+      qn += cnt;
     };
 
     // a row inside the frame for lanes whose rows run past it (re-read, masked)
@@ -709,9 +717,9 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     const uint8_t* tbase = a.frames + (int64_t)f * a.frame_stride + (int64_t)r0 * a.line_length;
     auto run = [&](auto full_c) {
       constexpr bool FULL = decltype(full_c)::value;
-      // One step: the chunk's 4 words.  All LDS lookups are issued before
-      // any queue write (the queue shares LDS, so the compiler keeps the
-      // order), then the selects, then the exception words are queued.
+      // One step: the chunk's 8 words.  All LDS lookups are issued before
+      // any record write (the queue shares LDS, so the compiler keeps the
+      // order), then the selects, then the two pieces' records.
       auto step = [&](const uint32_t (&cw)[CW], int s) {
         const bool valid = FULL || s < vsteps, validb = SPLIT ? (FULL || s < vstepsb) : valid;
         // lanes with a valid row (rows past the frame re-read a valid row:
@@ -724,52 +732,27 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         for (int i = 0; i < CW; ++i) c[i] = chroma_of(cw[i]);
 #pragma unroll
         for (int i = 0; i < CW; ++i) {
-#ifdef TRIK_AB_NO_LDS  // timing attribution only
-          d[i] = (c[i] * 0x9E37u) & 0xFFFFu;
-          cut[i] = 8u * (c[i] >> 12);
-#else
           d[i] = ld16(kLdsRuns + 2u * c[i]);
-#if TRIK_CHROMA_SPLITB
-          // the block c >> 4: its pair's palette offset and its cut, two bytes
-          const uint32_t b = c[i] >> 4;
-          pr[i] = ld8(kLdsBlkPair + b);
-          cut[i] = ld8(kLdsBlkCut + b);
-#else
           // the block word: the pair's palette offset | the cut << 8
           cut[i] = ld16(kLdsBlocks + ((c[i] >> 3) & 0x1FFEu));
           pr[i] = cut[i] & 0xFFu;
-#endif
-#endif
         }
-#ifdef TRIK_AB_NO_LDS
-#pragma unroll
-        for (int i = 0; i < CW; ++i) { mm[i].x = cut[i] & 0x01010101u; mm[i].y = (cut[i] >> 1) & 0x01010101u; }
-#else
 #pragma unroll
         for (int i = 0; i < CW; ++i) mm[i] = ld64(kLdsPairs + pr[i]);
-#endif
         // pin the descriptors as 32-bit values here (ds_read_u16 zero-extends):
         // otherwise the zero extension is sunk past the drain branches and
         // costs a v_and per word
 #pragma unroll
         for (int i = 0; i < CW; ++i) asm volatile("" : "+v"(d[i]), "+v"(cut[i]));
-        // per word: the selects, then the words with a pixel for the exact
-        // path (a wave mask in SGPRs) are queued
-        const uint32_t pos_s = x0 | ((uint32_t)(ro + s * g.rstep) << 16);
-        const uint32_t pos_b = pos_s + ((uint32_t)half << 16);
         uint64_t bal[CW];
 #pragma unroll
         for (int i = 0; i < CW; ++i) {
           uint64_t q0, q1;
-#ifdef TRIK_AB_STREAM  // timing attribution only: no detection at all
-          e[2 * i] = cw[i] & 0x01010101u;
-          e[2 * i + 1] = (cw[i] >> 1) & 0x01010101u;
-          q0 = q1 = 0;
-#else
-          select2<TRIK_CHROMA_SPLITB ? 0 : 1>(cw[i], d[i], cut[i], mm[i].x, mm[i].y, i < 4 ? vma : vmb, e[2 * i],
-                                              e[2 * i + 1], q0, q1);
-#endif
+          select2<1>(cw[i], d[i], cut[i], mm[i].x, mm[i].y, i < 4 ? vma : vmb, e[2 * i], e[2 * i + 1], q0, q1);
           bal[i] = q0 | q1;
+          // formed here, so the word's compare masks die here (sunk into the
+          // append branches they would all stay live in SGPRs)
+          asm volatile("" : "+s"(bal[i]));
           if (MASKS && (i < 4 ? valid : validb)) {  // verification mode: the exact path writes the flagged pixels
             const int y = y0 + s * g.rstep + (i < 4 ? 0 : half);
             uint8_t* mp = a.masks + ((int64_t)f * a.height + y) * a.width + x0 + xoff(i);
@@ -779,77 +762,21 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
             if (!__builtin_amdgcn_inverse_ballot_w64(q1)) mp[1] = a.mask_shift ? (uint8_t)(mp[1] | m1) : m1;
           }
         }
-#ifndef TRIK_AB_NO_ENQUEUE  // timing attribution only (drops the exception words)
-        // The words with a pixel for the exact path are appended to the
-        // wave's queue at their rank among the slot's flagged lanes.  (A branch
-        // on a slot's mask would seldom skip: some lane of the wave has a
-        // flagged word in most slots.)
-        auto rank = [](uint64_t m) {
-          return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        };
-#if TRIK_CHROMA_Q2
-        // pre[i]: the step's flagged words before slot i (one scalar prefix
-        // chain gives the ranks' bases and the step total)
-        uint32_t pre[CW + 1];
-        pre[0] = 0;
-#pragma unroll
-        for (int i = 0; i < CW; ++i) pre[i + 1] = pre[i] + (uint32_t)__builtin_popcountll(bal[i]);
-        const int total = (int)pre[CW];
-        // the whole step fits nearly always (qn < kDrainAt here, total ~15 of
-        // at most 512): one basic block of EXEC-masked stores, no branch and
-        // no drain check between the words; otherwise the queue is emptied
-        // first, and a step with more flagged words than the queue holds
-        // (never seen) stores word by word, emptying it after each
-        if (qn + total > kHotQueueCap)
-          while (qn > 0) drain_rare(qn < 64 ? qn : 64);
-        if (total <= kHotQueueCap) {
-          // entry index = the entries before this slot + the lane's rank (mbcnt
-          // accumulates the scalar count; measured faster than a v_lshl_add on
-          // an SGPR base, which waits for the SALU chain)
-          const uint32_t qtail = __builtin_amdgcn_readfirstlane(qbase_s + 8u * (uint32_t)qn);
-#pragma unroll
-          for (int i = 0; i < CW; ++i) {
-            // a slot no lane flagged skips its rank and store (one scalar
-            // branch): neutral at C3's 85 % flagged slots, -6 % at C4 and
-            // -4 % on scene frames (profiles/r02h_skip_ab.txt)
-            if (bal[i] == 0) continue;
-            const uint32_t idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[i] >> 32),
-                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bal[i], pre[i]));
-            store_masked(bal[i], qtail + 8u * idx, cw[i], (i < 4 ? pos_s : pos_b) + xoff(i));
-          }
-          qn += total;
-        } else {
-#pragma unroll
-          for (int i = 0; i < CW; ++i) {
-            const uint32_t qoff = __builtin_amdgcn_readfirstlane(qbase_s + 8u * (uint32_t)qn);
-            store_masked(bal[i], qoff + 8u * rank(bal[i]), cw[i], (i < 4 ? pos_s : pos_b) + xoff(i));
-            qn += __builtin_popcountll(bal[i]);
-            while (qn > 0) drain_rare(qn < 64 ? qn : 64);
-          }
-        }
-#ifdef TRIK_AB_NO_DRAIN  // timing attribution only (drops the exception words)
-        if (qn >= kDrainAt) qn = 0;
-#else
-        while (qn >= kDrainAt) drain(qn < 64 ? qn : 64);
-#endif
-#else
-#pragma unroll
-        for (int i = 0; i < CW; ++i) {
-          if (__builtin_amdgcn_inverse_ballot_w64(bal[i])) {
-            const uint32_t qa = __builtin_amdgcn_readfirstlane(qbase_s + 8u * (uint32_t)qn) + 8u * rank(bal[i]);
-            *(lds32_t)(uintptr_t)qa = cw[i];
-            *(lds32_t)(uintptr_t)(qa + 4u) = (i < 4 ? pos_s : pos_b) + xoff(i);
-          }
-          qn += __builtin_popcountll(bal[i]);
-#ifdef TRIK_AB_NO_DRAIN
-          if ((i & 1) && qn >= kDrainAt) qn = 0;
-#else
-          if (i & 1)
-            while (qn >= kDrainAt) drain(qn < 64 ? qn : 64);
-#endif
-        }
-#endif
-#endif
+        // per piece: the lanes with a flagged word (SALU) and the record's
+        // meta word with the flag bits (bit j = word j of the piece)
+        const uint64_t ma = bal[0] | bal[1] | bal[2] | bal[3];
+        const uint64_t mb = bal[4] | bal[5] | bal[6] | bal[7];
+        const uint32_t meta_a = meta_x | ((uint32_t)(ro + s * g.rstep) << 16);
+        const uint32_t fa = meta_a | lane_bit(bal[0], 1u) | lane_bit(bal[1], 2u) | lane_bit(bal[2], 4u) |
+                            lane_bit(bal[3], 8u);
+        const uint32_t fb = (meta_a + meta_b) | lane_bit(bal[4], 1u) | lane_bit(bal[5], 2u) | lane_bit(bal[6], 4u) |
+                            lane_bit(bal[7], 8u);
+        u32x4 wa, wb;
+        wa.x = cw[0]; wa.y = cw[1]; wa.z = cw[2]; wa.w = cw[3];
+        wb.x = cw[4]; wb.y = cw[5]; wb.z = cw[6]; wb.w = cw[7];
+        append(ma, wa, fa);
+        append(mb, wb, fb);
+        while (qn >= 64) drain(64);
 #pragma unroll
         for (int i = 0; i < CW; ++i) P[i] = P[i] + e[2 * i] + e[2 * i + 1];
 #pragma unroll
@@ -867,14 +794,11 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
             Ba += times(CumA);
             Bb += times(CumB);
             // group sums of the pair counters stay below 256 per byte
-            // (kGroup * 2 * kMaxSteps <= 255), so one split per group
-            constexpr int kGroup = CW == 8 ? 4 : 2;
+            // (4 * 2 * kMaxSteps <= 255), so one split per group
             CumS = CumA = CumB = 0;
 #pragma unroll
-            for (int g0 = 0; g0 < CW; g0 += kGroup) {
-              uint32_t G = 0;
-#pragma unroll
-              for (int i = g0; i < g0 + kGroup; ++i) G += P[i];
+            for (int g0 = 0; g0 < CW; g0 += 4) {
+              const uint32_t G = P[g0] + P[g0 + 1] + P[g0 + 2] + P[g0 + 3];
               CumS += G;
               CumA += G & 0x00FF00FFu;
               CumB += (G >> 8) & 0x00FF00FFu;
@@ -897,14 +821,14 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         return s < vstepsb ? pf + hb + (int64_t)s * rowstep : pf;
       };
       uint32_t wa[CW], wb[CW];
-      load_chunk<LAYOUT, CW>(row_ptr(0), row_ptr_b(0), plane, wa);
+      load_chunk<LAYOUT>(row_ptr(0), row_ptr_b(0), plane, wa);
       for (int s = 0; s < steps; s += 2) {
         if (FULL && s + 1 < steps) rb += rowstep;
-        load_chunk<LAYOUT, CW>(row_ptr(s + 1), row_ptr_b(s + 1), plane, wb);
+        load_chunk<LAYOUT>(row_ptr(s + 1), row_ptr_b(s + 1), plane, wb);
         step(wa, s);
         if (s + 1 >= steps) break;
         if (FULL && s + 2 < steps) rb += rowstep;
-        load_chunk<LAYOUT, CW>(row_ptr(s + 2), row_ptr_b(s + 2), plane, wa);
+        load_chunk<LAYOUT>(row_ptr(s + 2), row_ptr_b(s + 2), plane, wa);
         step(wb, s + 1);
       }
     };
@@ -940,28 +864,76 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
 #pragma unroll
     for (int v = 0; v < 12; ++v) red[v] = v < 3 * NR ? acc[v] : 0u;
     wave_sums12(red);
-    if ((lane & 15) == 15) {
-      // lane 16 r + 15 holds values 3 r .. 3 r + 2: range r's N, sum x, sum y
-      const int rr = lane >> 4;
-      if (rr < NR) {
-#if TRIK_CHROMA_Q2
-        // and the rare path's sums of this tile
-        const uint32_t ra = rare_s + 12u * (uint32_t)rr;
-#pragma unroll
-        for (int v = 0; v < 3; ++v) {
-          red[v] += *(lds32_t)(uintptr_t)(ra + 4u * v);
-          *(lds32_t)(uintptr_t)(ra + 4u * v) = 0u;
-        }
-#endif
+    // lane 16 r + 15 holds values 3 r .. 3 r + 2: range r's N, sum x, sum y
+    const int rr = lane >> 4;
+    if (!a.fused) {
+      if ((lane & 15) == 15 && rr < NR) {
         unsigned long long* dst =
             reinterpret_cast<unsigned long long*>(&a.sums[(int64_t)f * a.sums_ranges + a.range_offset + rr].points);
 #pragma unroll
         for (int v = 0; v < 3; ++v)
           if (red[v]) atomicAdd(dst + v, (unsigned long long)red[v]);
       }
+      continue;
+    }
+    // fused step: the wave's values go into the frame's LDS slot; the last
+    // wave to finish the frame's last tile stores its sums and targets and
+    // adds them to the workgroup's totals, then frees the slot for frame + 4
+    const uint32_t sb = kLdsFrames + (uint32_t)((f - f_first) & (kFrameSlots - 1)) * kFrameSlotBytes;
+    while (__builtin_amdgcn_readfirstlane(ld_acquire(sb + 100)) != (uint32_t)f) __builtin_amdgcn_s_sleep(2);
+    if ((lane & 15) == 15 && rr < NR) {
+#pragma unroll
+      for (int v = 0; v < 3; ++v) lds_add_u64(sb + 8u * (uint32_t)(3 * rr + v), red[v]);
+    }
+    uint32_t arrived = 0;
+    if (lane == 0) arrived = lds_add_rtn_u32(sb + 96, 1u);  // after this wave's adds (LDS is in order)
+    arrived = __builtin_amdgcn_readfirstlane(arrived);
+    if (arrived + 1 == (blockDim.x >> 6) * (uint32_t)g.tiles_per_frame) {
+      const int64_t o = (int64_t)f * a.sums_ranges + a.range_offset;
+      const bool mine = lane < 3 * NR;
+      const unsigned long long v = mine ? ld_u64(sb + 8u * (uint32_t)lane) : 0ull;
+      if (mine) {
+        reinterpret_cast<unsigned long long*>(&a.sums[o + lane / 3].points)[lane % 3] = v;
+        lds_add_u64(kLdsTotals + 8u * (uint32_t)lane, v);
+      }
+      if (a.targets && lane < NR)
+        a.targets[o + lane] = target_of(ld_u64(sb + 24u * (uint32_t)lane), ld_u64(sb + 24u * (uint32_t)lane + 8u),
+                                        ld_u64(sb + 24u * (uint32_t)lane + 16u), a.width, a.height);
+      if (lane < 12) st_u64(sb + 8u * (uint32_t)lane, 0ull);
+      if (lane == 0) {
+        *(lds32_t)(uintptr_t)(sb + 96) = 0u;
+        st_release(sb + 100, (uint32_t)(f + kFrameSlots));
+      }
     }
   }
+  // fused step: the per-target totals.  Every workgroup stores its totals; the
+  // last one to finish (a device-scope counter, reset by it for the next
+  // launch) sums them into a.totals.
+  if (!a.fused || !a.totals) return;
+  __syncthreads();
+  unsigned long long* part = a.wg_part + 12 * (int64_t)blockIdx.x;
+  if (t < 12) part[t] = ld_u64(kLdsTotals + 8u * (uint32_t)t);
+  __threadfence();
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t done = atomicAdd(a.wg_cnt, 1u);
+    *(lds32_t)(uintptr_t)(kLdsTotals + 96) = done + 1 == gridDim.x ? 1u : 0u;
+  }
+  if (t < 12) st_u64(kLdsTotals + 8u * (uint32_t)t, 0ull);
+  __syncthreads();
+  if (*(lds32_t)(uintptr_t)(kLdsTotals + 96) == 0u) return;
+  __threadfence();
+  for (uint32_t j = (uint32_t)t; j < 12u * gridDim.x; j += blockDim.x)
+    lds_add_u64(kLdsTotals + 8u * (j % 12u),
+                __hip_atomic_load(a.wg_part + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  __syncthreads();
+  if (t < 3 * NR)
+    reinterpret_cast<unsigned long long*>(&a.totals[a.range_offset + t / 3].points)[t % 3] =
+        ld_u64(kLdsTotals + 8u * (uint32_t)t);
+  if (t == 0) *a.wg_cnt = 0u;
 }
+
+
 
 
 // ---------------------------------------------------------------------------
@@ -1101,7 +1073,7 @@ __global__ __launch_bounds__(kMaxBlock) void blob_chroma_meta_kernel(BlobArgs a,
 
 template <int LAYOUT, int NR, bool MASKS>
 int launch_t(const KernelArgs& a, const ChromaGeom& g, const ChromaTables* ct, hipStream_t s) {
-  auto kern = chroma_kernel<LAYOUT, NR, MASKS, kChunkWords>;
+  auto kern = chroma_kernel<LAYOUT, NR, MASKS>;
   hipError_t e = set_dynamic_lds(reinterpret_cast<const void*>(kern), (int)kLdsBytes);
   if (e != hipSuccess) return e;
   const int cus = device_cus();
@@ -1179,10 +1151,18 @@ bool chroma_geometry_ok(const KernelArgs& a) {
   return chroma_geometry(a, g);
 }
 
+// The fused step hands each workgroup (one per CU) whole frames: at least 4
+// per workgroup keeps the imbalance of n_frames / CUs to a quarter frame.
+bool chroma_fused_ok(const KernelArgs& a) {
+  ChromaGeom g;
+  return !a.masks && chroma_geometry(a, g) && (int64_t)a.n_frames >= 4 * (int64_t)device_cus();
+}
+
 int launch_chroma(const KernelArgs& a, const ChromaTables* ct, bool write_masks, hipStream_t s) {
   ChromaGeom g;
   if (!chroma_geometry(a, g)) return hipErrorNotSupported;
   if (g.n_tiles == 0) return hipSuccess;
+  if (a.fused && (write_masks || !chroma_fused_ok(a) || !a.wg_part || !a.wg_cnt)) return hipErrorInvalidValue;
   if (a.layout == TRIK_HSV_LAYOUT_YUYV)
     return write_masks ? launch_nr<TRIK_HSV_LAYOUT_YUYV, true>(a, g, ct, s)
                        : launch_nr<TRIK_HSV_LAYOUT_YUYV, false>(a, g, ct, s);

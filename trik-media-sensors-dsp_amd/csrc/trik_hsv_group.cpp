@@ -45,6 +45,9 @@ struct Rccl {
   decltype(&ncclCommInitAll) comm_init_all = nullptr;
   decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclCommAbort) comm_abort = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
   std::string error;  // why loading failed ("" when loaded)
 };
@@ -70,6 +73,9 @@ const Rccl& rccl() {
     sym("ncclCommInitAll", r.comm_init_all);
     sym("ncclAllReduce", r.all_reduce);
     sym("ncclCommDestroy", r.comm_destroy);
+    sym("ncclCommAbort", r.comm_abort);
+    sym("ncclGroupStart", r.group_start);
+    sym("ncclGroupEnd", r.group_end);
     sym("ncclGetErrorString", r.error_string);
   });
   return r;
@@ -149,6 +155,10 @@ struct TrikHsvGroup {
   std::vector<ncclComm_t> comms;
   std::vector<std::unique_ptr<Worker>> workers;
   std::mutex mu;  // one group call at a time
+  // a collective failed to enqueue on some device: the communicators were
+  // aborted (peers that had enqueued theirs do not wait forever) and the
+  // group only accepts trik_hsv_group_delete (and _sync) from then on
+  bool broken = false;
 
   // Runs job(d) on every device's worker (its device current) and waits;
   // the first failure is reported on the calling thread.
@@ -172,6 +182,18 @@ struct TrikHsvGroup {
       }
     }
     return rc ? set_error(rc, first) : 0;
+  }
+
+  // Aborts every communicator: RCCL kernels already enqueued return, so the
+  // streams drain.
+  void abort_comms() {
+    for (size_t d = 0; d < comms.size(); ++d)
+      if (comms[d]) {
+        (void)hipSetDevice(devices[d]);
+        (void)rccl().comm_abort(comms[d]);
+        comms[d] = nullptr;
+      }
+    broken = true;
   }
 
   void release() {
@@ -244,30 +266,51 @@ extern "C" int32_t trik_hsv_group_process(TRIK_HSV_GroupHandle g, const TrikHsvF
   for (size_t d = 0; d < g->devices.size(); ++d)
     if (!totals[d]) return set_error(TRIK_IVIDTRANSCODE_EFAIL, "group_process: totals_dev[" + std::to_string(d) + "] is NULL");
   std::lock_guard<std::mutex> lock(g->mu);
-  // 1. every device: its shard, then the totals of its frames (all enqueued
-  //    before any collective, so a failure cannot leave an all-reduce waiting)
+  if (g->broken) return set_error(TRIK_IVIDTRANSCODE_EFAIL, "group_process: a collective failed earlier; delete the group");
+  // 1. every device, on its worker thread: its shard, then the totals of its
+  //    frames (all enqueued before any collective: a failure here returns
+  //    before any device has an all-reduce waiting for its peers)
   int32_t rc = g->each([&](int d) -> int32_t {
     const TrikHsvFrameBatch& b = batches[d];
     hipStream_t s = g->streams[d];
-    if (b.n_frames > 0) {
-      int32_t r = trik_hsv_process_batch(g->handles[d], &b, ranges, n, sums[d], targets ? targets[d] : nullptr, s);
-      if (r) return r;
-    }
-    return trik_hsv_batch_totals(b.n_frames > 0 ? b.n_frames : 0, n, sums[d], totals[d], s);
+    if (b.n_frames > 0)  // the full step: one launch per 4 ranges where the fused step applies
+      return trik_hsv_process_batch_totals(g->handles[d], &b, ranges, n, sums[d], targets ? targets[d] : nullptr,
+                                           totals[d], s);
+    return trik_hsv_batch_totals(0, n, sums[d], totals[d], s);
   });
   if (rc) return rc;
-  // 2. one all-reduce of n x 3 int64 over the devices (one thread per device,
-  //    one communicator each)
-  return g->each([&](int d) -> int32_t {
-    const ncclResult_t e = rccl().all_reduce(totals[d], totals[d], (size_t)3 * n, ncclInt64, ncclSum, g->comms[d],
-                                             g->streams[d]);
-    return e == ncclSuccess ? 0 : nccl_fail("ncclAllReduce", e);
-  });
+  // 2. one all-reduce of n x 3 int64 over the devices, issued from this
+  //    thread as one RCCL group (the single-process multi-device pattern:
+  //    every device's part is enqueued together or the group fails).  If it
+  //    fails, the communicators are aborted so that no device's part waits
+  //    for a peer that never joined, and the group is marked broken.
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  ncclResult_t e = rccl().group_start();
+  const char* what = "ncclGroupStart";
+  const bool started = e == ncclSuccess;
+  for (size_t d = 0; e == ncclSuccess && d < g->devices.size(); ++d) {
+    e = rccl().all_reduce(totals[d], totals[d], (size_t)3 * n, ncclInt64, ncclSum, g->comms[d], g->streams[d]);
+    what = "ncclAllReduce";
+  }
+  if (started) {  // a started group is always ended
+    const ncclResult_t e2 = rccl().group_end();
+    if (e == ncclSuccess && e2 != ncclSuccess) {
+      e = e2;
+      what = "ncclGroupEnd";
+    }
+  }
+  (void)hipSetDevice(prev);
+  if (e == ncclSuccess) return 0;
+  g->abort_comms();
+  return nccl_fail(what, e);
 }
 
 extern "C" int32_t trik_hsv_group_sync(TRIK_HSV_GroupHandle g) {
   if (!g) return set_error(TRIK_IVIDTRANSCODE_EFAIL, "group is NULL");
   std::lock_guard<std::mutex> lock(g->mu);
+  // (after a failed collective the aborted communicators' kernels have
+  // returned, so this does not block on them)
   return g->each([&](int d) -> int32_t {
     const hipError_t e = hipStreamSynchronize(g->streams[d]);
     return e == hipSuccess ? 0 : set_error(TRIK_IVIDTRANSCODE_EFAIL, std::string("hipStreamSynchronize: ") + hipGetErrorString(e));

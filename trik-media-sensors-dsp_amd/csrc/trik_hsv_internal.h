@@ -133,7 +133,37 @@ struct KernelArgs {
   const unsigned long long* gate = nullptr;
   unsigned long long gate_max = 0;
   int32_t gate_le = 0;
+  // The fused step (chroma-run kernel; chroma_fused_ok): whole frames per
+  // workgroup, so a frame's sums are complete inside one workgroup and are
+  // stored, not added (no zeroing); the same launch writes the targets and
+  // the per-target batch totals (the last workgroup sums the workgroups'
+  // partial totals).  DESIGN.md section 4.5.
+  int32_t fused = 0;
+  TrikHsvTarget* targets = nullptr;       // [n_frames][sums_ranges], or NULL
+  TrikHsvTargetSums* totals = nullptr;    // [sums_ranges], or NULL
+  unsigned long long* wg_part = nullptr;  // scratch: [workgroups][12]
+  uint32_t* wg_cnt = nullptr;             // scratch: 0 between launches
 };
+
+// The target of one (frame, range) from its sums: WSEQ:486-505 (unsigned
+// centroid division, fp32 sqrtf / ceil radius).  The reference's int32 /
+// uint32 arithmetic: the sums are non-negative, so 64-bit division agrees
+// wherever the reference's 32-bit accumulators do not overflow, and stays
+// exact beyond.
+__device__ __forceinline__ TrikHsvTarget target_of(uint64_t points, uint64_t sum_x, uint64_t sum_y, int width,
+                                                   int height) {
+  TrikHsvTarget r = {0, 0, 0, 0};
+  if (points > 0) {
+    const int32_t cx = (int32_t)(sum_x / points);
+    const int32_t cy = (int32_t)(sum_y / points);
+    const float q = __fdiv_rn((float)(uint32_t)points, 3.1415927f);
+    const uint32_t radius = (uint32_t)ceilf(__fsqrt_rn(q));  // WSEQ:492
+    r.x = (int8_t)(((cx - width / 2) * 100 * 2) / width);   // WSEQ:496-498
+    r.y = (int8_t)(((cy - height / 2) * 100 * 2) / height);
+    r.size = (uint8_t)((uint32_t)(radius * 100 * 4) / (uint32_t)(width + height));
+  }
+  return r;
+}
 
 __device__ __forceinline__ bool gated_out(const unsigned long long* gate, unsigned long long gate_max, int gate_le) {
   return gate && ((*gate <= gate_max) != (gate_le != 0));
@@ -206,6 +236,9 @@ int launch_stripe(const KernelArgs& a, bool write_masks, hipStream_t s);
 // another kernel.
 int build_chroma_tables(const RangeTables* t, ChromaTables* ct, hipStream_t s);
 bool chroma_geometry_ok(const KernelArgs& a);
+// the fused step applies (frames whole per workgroup, >= 4 frames each; no
+// verification masks)
+bool chroma_fused_ok(const KernelArgs& a);
 int launch_chroma(const KernelArgs& a, const ChromaTables* ct, bool write_masks, hipStream_t s);
 // Sets the calling thread's trik_hsv_last_error() message; returns code.
 int32_t set_error(int32_t code, const std::string& msg);

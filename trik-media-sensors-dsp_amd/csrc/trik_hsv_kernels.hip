@@ -125,6 +125,7 @@ __device__ __forceinline__ void load_chunk(const uint8_t* fr, int64_t row_off, i
 template <int LAYOUT, int NR, bool MASKS, bool ALIGNED>
 __global__ __launch_bounds__(kBlock) void reduce_kernel(KernelArgs a, int64_t n_tiles,
                                                         int band, int tiles_per_frame) {
+  if (gated_out(a.gate, a.gate_max, a.gate_le)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   RangeTables& tab = *reinterpret_cast<RangeTables*>(lds);
   uint64_t* scratch = reinterpret_cast<uint64_t*>(lds + sizeof(RangeTables));
@@ -190,21 +191,7 @@ __global__ void targets_kernel(int n, int width, int height, const TrikHsvTarget
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const TrikHsvTargetSums s = sums[i];
-  TrikHsvTarget r = {0, 0, 0, 0};
-  const uint64_t points = (uint64_t)s.points;
-  if (points > 0) {
-    // int32 / uint32 in the reference (unsigned division, WSEQ:488-489); the
-    // sums are non-negative so 64-bit division agrees wherever the reference's
-    // 32-bit accumulators do not overflow, and stays exact beyond.
-    const int32_t cx = (int32_t)((uint64_t)s.sum_x / points);
-    const int32_t cy = (int32_t)((uint64_t)s.sum_y / points);
-    const float q = __fdiv_rn((float)(uint32_t)points, 3.1415927f);
-    const uint32_t radius = (uint32_t)ceilf(__fsqrt_rn(q));  // WSEQ:492
-    r.x = (int8_t)(((cx - width / 2) * 100 * 2) / width);   // WSEQ:496-498
-    r.y = (int8_t)(((cy - height / 2) * 100 * 2) / height);
-    r.size = (uint8_t)((uint32_t)(radius * 100 * 4) / (uint32_t)(width + height));
-  }
-  out[i] = r;
+  out[i] = target_of((uint64_t)s.points, (uint64_t)s.sum_x, (uint64_t)s.sum_y, width, height);
 }
 
 // ---------------------------------------------------------------------------

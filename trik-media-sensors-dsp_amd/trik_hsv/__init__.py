@@ -73,6 +73,7 @@ def _batch(frames, width, height, line_length, layout, n_frames=None, frame_stri
 
 
 HOT_AUTO, HOT_STRIPE, HOT_CHROMA, HOT_GENERIC = 0, 1, 2, 3
+HOT_MIXED = 4  # last_hot_kernel(): the call's groups of 4 ranges ran different kernels
 
 
 class _HotKernel:
@@ -141,6 +142,29 @@ class Detector(_HotKernel):
         if rc:
             raise TrikHsvError(rc, "trik_hsv_process_batch")
         return sums, targets
+
+    def process_batch_totals(self, frames, width, height, line_length, layout, ranges, *, n_frames=None,
+                             frame_stride=None, stream=None, sums=None, targets=None, totals=None):
+        """The full step (trik_hsv_process_batch_totals): sums, targets and the
+        per-target batch totals; one launch per group of 4 ranges where the
+        chroma-run kernel runs on >= 4 frames per CU.  Returns (sums, targets,
+        totals int64 [T,3])."""
+        import torch
+
+        b = _batch(frames, width, height, line_length, layout, n_frames, frame_stride)
+        arr, T = _ranges(ranges)
+        if sums is None:
+            sums = torch.empty((b.n_frames, T, 3), dtype=torch.int64, device=frames.device)
+        if targets is None:
+            targets = torch.empty((b.n_frames, T, 4), dtype=torch.int8, device=frames.device)
+        if totals is None:
+            totals = torch.empty((T, 3), dtype=torch.int64, device=frames.device)
+        rc = _lib.trik_hsv_process_batch_totals(self._h, C.byref(b), arr, T, C.c_void_p(sums.data_ptr()),
+                                                C.c_void_p(targets.data_ptr()), C.c_void_p(totals.data_ptr()),
+                                                _stream_ptr(stream, frames))
+        if rc:
+            raise TrikHsvError(rc, "trik_hsv_process_batch_totals")
+        return sums, targets, totals
 
     def batch_sums(self, frames, width, height, line_length, layout, ranges, sums, *,
                    n_frames=None, frame_stride=None, stream=None):

@@ -180,6 +180,8 @@ PROTOTYPES = {
     "trik_hsv_last_error": ([], C.c_char_p),
     "trik_hsv_process_batch": ([C.c_void_p, C.POINTER(FrameBatch), C.POINTER(InArgsAlg), i32,
                                 C.c_void_p, C.c_void_p, C.c_void_p], i32),
+    "trik_hsv_process_batch_totals": ([C.c_void_p, C.POINTER(FrameBatch), C.POINTER(InArgsAlg), i32,
+                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], i32),
     "trik_hsv_batch_sums": ([C.c_void_p, C.POINTER(FrameBatch), C.POINTER(InArgsAlg), i32,
                              C.c_void_p, C.c_void_p], i32),
     "trik_hsv_batch_targets": ([C.POINTER(FrameBatch), i32, C.c_void_p, C.c_void_p,
