@@ -3,9 +3,15 @@
 Workload (BASELINE.json configs[2], "C3"): 4096 frames x 640x480 packed YUYV
 per GPU, 4 HSV target ranges, frames synthesised on the device (SplitMix64
 uniform bytes) before the timed region, so inputs are resident in HBM.  A
-step = one full pass of the hot path over the batch: zero the per-frame sums,
-the fused detect + reduce kernel, the target epilogue kernel, and the
-per-target batch totals (RCCL all-reduce across GPUs when N > 1).
+step = one full pass of the hot path over the batch
+(trik_hsv_process_batch_totals): every frame's sums, its targets (the
+epilogue) and the per-target batch totals -- one launch of the chroma-run
+kernel at this size (the fused step) -- then the RCCL all-reduce of the totals
+across GPUs when N > 1.
+
+Before the warmup (untimed for `value`, reported in their own fields): the
+first call of a fresh handle, a batch with a new range set (cold_batch), and
+the same step on scene frames (`scene`).
 
 With N GPUs (torch.distributed.run, one process per GPU) each rank owns its
 own 4096 frames (global frames rank*4096 ...): weak scaling; at N = 8 this is
@@ -48,8 +54,7 @@ def workload_name(wl, per_gpu, total, world, w, h, t):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # 0.7 ms per step: 50 warmup steps bring the clocks to steady state (20
-    # steps after 3 warmups read ~10 % slow), 200 timed steps take 0.14 s
+    # 0.6 ms per step: 200 timed steps take 0.12 s
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3",
@@ -61,15 +66,21 @@ def parse():
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--targets", type=int, default=None)
     ap.add_argument("--kind", type=int, default=0, help="0 uniform random bytes, 1 scene")
-    ap.add_argument("--cpu-frames", type=int, default=1024, help="CPU baseline sample (frames)")
+    ap.add_argument("--cpu-frames-all", type=int, default=4096,
+                    help="CPU baseline sample on every allowed hardware thread (frames)")
+    ap.add_argument("--cpu-frames", type=int, default=1024, help="CPU sample on the per-GPU CPU share (frames)")
+    ap.add_argument("--scene-launches", type=int, default=20,
+                    help="launches timed on scene frames before the warmup (0: none)")
     ap.add_argument("--cpu-frames-1core", type=int, default=64, help="single-thread CPU sample")
     ap.add_argument("--cpu-frames-emul", type=int, default=32,
                     help="sample of the oracle's intrinsic-level emulation (secondary rate)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the cold-batch and scene measurements (PMC passes: only the bench's own launches)")
     ap.add_argument("--hot", choices=["auto", "stripe", "chroma"], default="auto",
                     help="hot kernel (auto = the library's choice: chroma-run for this batch size)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
-                    help="rocprofv3 FETCH_SIZE summary used for roofline.traffic")
+                    help="rocprofv3 FETCH_SIZE summary used for roofline.traffic (when measured on these sources)")
     args = ap.parse_args()
     for k, v in WORKLOADS[args.workload].items():
         if getattr(args, k) is None:
@@ -77,13 +88,15 @@ def parse():
     return args
 
 
-def cpu_baseline(args, width, height, ll, n_ranges, gpu_sums):
-    """CPU baseline on a bounded sample of the same frames: the clean-room scalar
-    restatement of the path (oracle/trik_cpu_baseline.c, a plain CPU port:
-    closed-form arithmetic, frames over POSIX threads), checked against the GPU
-    sums of those frames.  Threads: this process's CPU share (affinity and
-    OMP_NUM_THREADS; 16 per GPU on the bench box) -- the machine's total is
-    reported beside it, not used."""
+def cpu_baseline(args, width, height, ll, n_ranges, host, gpu_sums):
+    """CPU baseline on a bounded sample of the same frames (host: the GPU
+    batch's bytes): the clean-room scalar restatement of the path
+    (oracle/trik_cpu_baseline.c, a plain CPU port: closed-form arithmetic,
+    frames over POSIX threads), checked against the GPU sums of those frames.
+    `value`: every hardware thread this process may run on (SURVEY 8(d):
+    hardware_concurrency over the affinity mask); beside it the box's per-GPU
+    CPU share (OMP_NUM_THREADS, 16 on the bench box), one thread, and the
+    oracle's intrinsic-level emulation."""
     import numpy as np
 
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -94,28 +107,34 @@ def cpu_baseline(args, width, height, ll, n_ranges, gpu_sums):
         allowed = len(os.sched_getaffinity(0))
     except AttributeError:
         allowed = machine
-    omp = int(os.environ.get("OMP_NUM_THREADS", allowed))
-    cores = max(1, min(allowed, omp))
-    n = min(args.cpu_frames, args.frames)
-    host = oracle.synth(n, width, height, ll, oracle.LAYOUT_YUYV, args.kind, SEED)
+    share = max(1, min(allowed, int(os.environ.get("OMP_NUM_THREADS", allowed))))
     rs = RANGES[:n_ranges]
-    t0 = time.perf_counter()
-    sums = oracle.cpu_batch(host, height * ll, n, width, height, ll, oracle.LAYOUT_YUYV, rs, n_threads=cores)
-    dt = time.perf_counter() - t0
+    fb = height * ll
+    px = width * height
+
+    def run(n, threads):
+        t0 = time.perf_counter()
+        out = oracle.cpu_batch(host, fb, n, width, height, ll, oracle.LAYOUT_YUYV, rs, n_threads=threads)
+        return out, time.perf_counter() - t0
+
+    n_all = min(args.cpu_frames_all, args.frames)
+    sums_all, dt_all = run(n_all, allowed)
+    n = min(args.cpu_frames, args.frames)
+    sums, dt = run(n, share)
     n1 = min(args.cpu_frames_1core, n)
-    t1 = time.perf_counter()
-    oracle.cpu_batch(host, height * ll, n1, width, height, ll, oracle.LAYOUT_YUYV, rs, n_threads=1)
-    dt1 = time.perf_counter() - t1
+    _, dt1 = run(n1, 1)
     ne = min(args.cpu_frames_emul, n)
     t2 = time.perf_counter()
-    emul, _ = oracle.batch(host, height * ll, ne, width, height, ll, oracle.LAYOUT_YUYV, rs, n_threads=cores)
+    emul, _ = oracle.batch(host, fb, ne, width, height, ll, oracle.LAYOUT_YUYV, rs, n_threads=share)
     dt2 = time.perf_counter() - t2
-    parity = bool(np.array_equal(sums, gpu_sums[:n])) and bool(np.array_equal(emul, gpu_sums[:ne]))
-    px = width * height
-    return {"value": round(n * px / dt / 1e6, 3), "unit": "Mpix/s", "cores": cores, "kind": "port",
+    parity = (bool(np.array_equal(sums_all, gpu_sums[:n_all])) and bool(np.array_equal(sums, gpu_sums[:n]))
+              and bool(np.array_equal(emul, gpu_sums[:ne])))
+    return {"value": round(n_all * px / dt_all / 1e6, 3), "unit": "Mpix/s", "cores": allowed, "kind": "port",
             "port": "clean-room scalar C restatement (oracle/trik_cpu_baseline.c), POSIX threads",
-            "sample": f"{n} frames x {width}x{height} YUYV, {n_ranges} ranges "
-                      f"(frames 0..{n - 1} of the GPU batch), {cores} threads, {dt:.2f} s",
+            "sample": f"{n_all} frames x {width}x{height} YUYV, {n_ranges} ranges "
+                      f"(frames 0..{n_all - 1} of the GPU batch), {allowed} threads, {dt_all:.2f} s",
+            "value_share": round(n * px / dt / 1e6, 3), "share_threads": share,
+            "share_sample": f"{n} frames, {share} threads (the box's CPU share per GPU), {dt:.2f} s",
             "value_1core": round(n1 * px / dt1 / 1e6, 3),
             "machine_threads": machine, "threads_allowed": allowed,
             "value_intrinsic_emulation": round(ne * px / dt2 / 1e6, 3),
@@ -133,15 +152,37 @@ def cpu_model():
     return "unknown"
 
 
+def source_digest():
+    """SHA-256 (16 hex) of the library's sources (csrc/ and the public header):
+    what a committed PMC pass was measured on (scripts/pmc_summary.py)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    src = os.path.join(ROOT, "trik-media-sensors-dsp_amd", "csrc")
+    for name in sorted(os.listdir(src)):
+        if name.endswith((".hip", ".cpp", ".h")):
+            with open(os.path.join(src, name), "rb") as f:
+                h.update(name.encode() + b"\0" + f.read())
+    with open(os.path.join(ROOT, "include", "trik_hsv.h"), "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def load_traffic(path, bytes_per_launch):
+    """(HBM read bytes per launch, where it comes from): the committed PMC pass
+    when it was measured at this algorithmic size on these sources, else None."""
+    rel = os.path.relpath(path, ROOT)
     try:
         with open(path) as f:
             pmc = json.load(f)
-        if pmc.get("bytes_per_launch_algorithmic") == bytes_per_launch:
-            return pmc.get("hbm_read_bytes_per_launch")
     except (OSError, ValueError):
-        pass
-    return None
+        return None, f"none: {rel} missing"
+    if pmc.get("bytes_per_launch_algorithmic") != bytes_per_launch:
+        return None, f"none: {rel} was measured at another size"
+    if pmc.get("source_digest") != source_digest():
+        return None, f"none: {rel} was measured on other sources ({pmc.get('source_digest')})"
+    return pmc.get("hbm_read_bytes_per_launch"), (f"committed PMC pass, {rel} (FETCH_SIZE x 2, "
+                                                  f"{pmc.get('measured', 'rocprofv3 --pmc')}; same sources)")
 
 
 def main():
@@ -181,41 +222,79 @@ def main():
     frames = torch.empty(max(F, 1) * fb, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
     trik_hsv.synth(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, args.kind, SEED, first_frame=first)
-    det = trik_hsv.Detector(hot={"auto": trik_hsv.HOT_AUTO, "stripe": trik_hsv.HOT_STRIPE,
-                                 "chroma": trik_hsv.HOT_CHROMA}[args.hot])
+    hot = {"auto": trik_hsv.HOT_AUTO, "stripe": trik_hsv.HOT_STRIPE, "chroma": trik_hsv.HOT_CHROMA}[args.hot]
+    det = trik_hsv.Detector(hot=hot)
     sums = torch.zeros((F, T, 3), dtype=torch.int64, device=dev)
+    targets = torch.zeros((F, T, 4), dtype=torch.int8, device=dev)
+    totals = torch.zeros((T, 3), dtype=torch.int64, device=dev)
 
-    def step(ev0=None, ev1=None):
-        sums.zero_()
+    def full_step(buf, rs, ev0=None, ev1=None):
+        """trik_hsv_process_batch_totals: sums, targets and totals of the batch
+        (one chroma-run launch where the fused step applies), events around it."""
         if ev0 is not None:
             ev0.record(stream)
-        det.batch_sums(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, ranges, sums, stream=stream)
+        det.process_batch_totals(buf, W, H, ll, trik_hsv.LAYOUT_YUYV, rs, n_frames=F, frame_stride=fb,
+                                 sums=sums, targets=targets, totals=totals, stream=stream)
         if ev1 is not None:
             ev1.record(stream)
-        targets = trik_hsv.batch_targets(sums, W, H, stream=stream)
-        totals = trik_hsv.batch_totals_device(sums, stream=stream)  # totals_kernel (C ABI)
+
+    def step(ev0=None, ev1=None):
+        full_step(frames, ranges, ev0, ev1)
         if backend == "nccl":
             all_reduce_totals(totals)  # RCCL over xGMI when N > 1: 3*T int64 per step
         elif world > 1:  # gloo rehearsal: reduce a host copy
             totals.copy_(all_reduce_totals(totals.cpu()))
-        return targets
 
     def timed_call(rs):
-        """GPU time (HIP events on the stream) and host time of one batch_sums call."""
+        """GPU time (HIP events on the stream) and host time of one full step."""
         c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        sums.zero_()
         torch.cuda.synchronize()
         c0.record(stream)
         h0 = time.perf_counter()
-        det.batch_sums(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, rs, sums, stream=stream)
+        full_step(frames, rs)
         host_ms = (time.perf_counter() - h0) * 1e3
         c1.record(stream)
         torch.cuda.synchronize()
         return c0.elapsed_time(c1), host_ms
 
+    # --- untimed for `value`, before the warmup ---------------------------
     # the first call of a fresh handle: table memory allocated, range tables
     # compiled on the host and uploaded, chroma-run tables built on the device
     first_ms, first_host_ms = timed_call(ranges)
+    # a range set the handle has not seen, on a warm handle (its table slots
+    # already allocated): what a workload that changes ranges pays per change.
+    # The host call only enqueues (no wait on the device).
+    def shifted(j):
+        return [(r[0] + j if k == 0 else r[0],) + tuple(r[1:]) for k, r in enumerate(ranges)]
+    new_ms = new_host_ms = warm_ms = float("nan")
+    if not args.no_extras:
+        for j in range(1, 5):  # fill the handle's table slots (4) with other sets
+            timed_call(shifted(j))
+        new_ms, new_host_ms = timed_call(shifted(5))
+        warm_ms, _ = timed_call(shifted(5))  # the same set again: its steady cost
+        timed_call(ranges)  # back to the bench set (rebuilt)
+    # scene frames (SURVEY 8(d)(ii)): camera-like content, the same step
+    scene = None
+    if args.scene_launches > 0 and not args.no_extras:
+        sframes = torch.empty_like(frames)
+        trik_hsv.synth(sframes, W, H, ll, trik_hsv.LAYOUT_YUYV, 1, SEED, first_frame=first)
+        full_step(sframes, ranges)
+        sev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.scene_launches)]
+        torch.cuda.synchronize()
+        for a, b in sev:
+            full_step(sframes, ranges, a, b)
+        torch.cuda.synchronize()
+        scene_ms = sorted(a.elapsed_time(b) for a, b in sev)
+        scene_avg = sum(scene_ms) / len(scene_ms)
+        del sframes
+        scene = {"kernel_ms": round(scene_avg, 4), "kernel_ms_median": round(scene_ms[len(scene_ms) // 2], 4),
+                 "frac": round(F * fb / (scene_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                 "mpix_per_s": round(F * W * H / (scene_avg / 1e3) / 1e6, 1), "launches": args.scene_launches,
+                 "data": "synthetic: device scene generator (gradients + 6 discs), seed 0x7A1C",
+                 "note": "the same full step on scene frames, timed before the warmup (not in `value`)"}
+
+    # --- the timed steps ----------------------------------------------------
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -232,17 +311,11 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
-    # a range set the handle has not seen, on a warm handle (its table slots
-    # already allocated): what a workload that changes ranges pays per change.
-    # The host call only enqueues (no wait on the device).
-    def shifted(j):
-        return [(r[0] + j if k == 0 else r[0],) + tuple(r[1:]) for k, r in enumerate(ranges)]
-    for j in range(1, 5):  # fill the handle's table slots (4) with other sets
-        timed_call(shifted(j))
-    new_ms, new_host_ms = timed_call(shifted(5))
-    timed_call(ranges)  # back to the bench set (rebuilt)
+    kind = det.last_hot_kernel()
     kname = {trik_hsv.HOT_CHROMA: "chroma_kernel", trik_hsv.HOT_STRIPE: "stripe_kernel",
-             trik_hsv.HOT_GENERIC: "reduce_kernel"}.get(det.last_hot_kernel(), "?")
+             trik_hsv.HOT_GENERIC: "reduce_kernel", trik_hsv.HOT_MIXED: "mixed"}.get(kind, "?")
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    fused = kind == trik_hsv.HOT_CHROMA and F >= 4 * cus
 
     el = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:
@@ -258,6 +331,7 @@ def main():
     value = px_total / elapsed / 1e6
     bytes_per_launch = F * fb  # algorithmic: 2 B/pixel read once
     achieved = bytes_per_launch / (kern_ms / 1e3) / 1e9
+    traffic, traffic_source = load_traffic(args.pmc, bytes_per_launch)
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "Mpix/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
@@ -271,20 +345,30 @@ def main():
                    "targets": T, "layout": "yuyv", "parallelism": f"dp{world} (frame shards)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": load_traffic(args.pmc, bytes_per_launch),
+                     "traffic": traffic, "traffic_source": traffic_source,
                      "kernel": f"{kname}<YUYV,{T}>", "kernel_ms": round(kern_ms, 4),
                      "kernel_ms_max_rank": round(kern_ms_max, 4),
+                     "kernel_scope": ("the step's one launch (fused: sums stored, targets and totals written "
+                                      "by the same kernel)" if fused else
+                                      "the step's launches (zero the sums, hot kernel, epilogue, totals)"),
                      "bytes_per_launch": bytes_per_launch},
-        # a batch with a new range set (not in `value`)
-        "cold_batch": {"cold_batch_ms": round(new_ms, 4), "table_build_ms": round(new_ms - kern_ms, 4),
+    }
+    if not args.no_extras:
+        out["cold_batch"] = {"cold_batch_ms": round(new_ms, 4), "table_build_ms": round(new_ms - warm_ms, 4),
+                       "warm_same_set_ms": round(warm_ms, 4),
                        "host_call_ms": round(new_host_ms, 4),
                        "first_call_ms": round(first_ms, 4), "first_call_host_ms": round(first_host_ms, 4),
-                       "note": "cold_batch_ms: one batch with a range set new to a warm handle (tables "
+                       "note": "cold_batch_ms: one step with a range set new to a warm handle (tables "
                                "compiled, uploaded and built on the device, then the hot kernel); "
-                               "first_call: a fresh handle, table memory allocated too"},
-    }
+                               "table_build_ms = cold_batch_ms - the same set's next step; "
+                               "first_call: a fresh handle, table memory allocated too; measured before "
+                               "the warmup"}
+    if scene is not None:
+        out["scene"] = scene
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb, parity = cpu_baseline(args, W, H, ll, T, sums.cpu().numpy())
+        n_host = min(F, max(args.cpu_frames_all, args.cpu_frames))
+        host = frames[: n_host * fb].cpu().numpy()
+        cb, parity = cpu_baseline(args, W, H, ll, T, host, sums.cpu().numpy())
         out["cpu_baseline"] = cb
         out["cpu_sample_parity"] = parity
     if rank == 0:

@@ -519,6 +519,14 @@ int32_t trik_hsv_set_hot_kernel(TRIK_VIDTRANSCODE_CV_Handle handle, int32_t kind
  * 4 ranges), or -1 when its tables are not built.  Waits for the builder's
  * readback if it is still in flight.  Returns 0 or TRIK_IVIDTRANSCODE_EFAIL. */
 int32_t trik_hsv_chroma_share(TRIK_VIDTRANSCODE_CV_Handle handle, double* share);
+/* The share of words the chroma-run kernel's exact path actually resolved on
+ * the handle's recent AUTO batches of that range set (the maximum over its
+ * groups; -1 before two readbacks have landed).  AUTO reads the kernel's
+ * counter back every few launches without waiting and sends a group whose
+ * measured share exceeds TRIK_HSV_CHROMA_MAX_SHARE -- input concentrated on
+ * the chromas its tables describe worst -- to the stripe kernel, trying the
+ * chroma-run kernel again every 32 batches.  Waits for a readback in flight. */
+int32_t trik_hsv_chroma_measured_share(TRIK_VIDTRANSCODE_CV_Handle handle, double* share);
 /* The kernel the handle's last hot call ran (TRIK_HSV_HOT_STRIPE, _CHROMA or
  * _GENERIC; TRIK_HSV_HOT_MIXED when its groups of 4 ranges ran different
  * kernels; 0 before any).  When the device chose (see above) this waits for

@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 OUT="$GRAFT_REPO_ROOT/gpurun_out"
 TAG="${1:-pmc}"
 shift || true
-ARGS="${*:---steps 3 --warmup 1 --no-cpu-baseline}"
+ARGS="${*:---steps 3 --warmup 1 --no-cpu-baseline --no-extras}"
 mkdir -p "$OUT/$TAG"
 cd /tmp && export TMPDIR=/tmp
 i=0

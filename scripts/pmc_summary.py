@@ -32,9 +32,13 @@ def main():
     if not vals:
         sys.exit(f"no dispatches of {kern!r} under {pmc_dir}")
     avg = {k: sum(v) / len(v) for k, v in vals.items()}
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import source_digest  # the sources these passes ran (bench.py checks it)
+
     res = {"kernel": sorted(names)[0], "dispatches_per_counter": {k: len(v) for k, v in vals.items()},
            "counters_avg_per_launch": {k: round(v, 1) for k, v in sorted(avg.items())},
-           "bytes_per_launch_algorithmic": alg}
+           "bytes_per_launch_algorithmic": alg, "source_digest": source_digest(),
+           "measured": f"rocprofv3 --pmc, one counter group per run, {os.path.basename(os.path.normpath(pmc_dir))}"}
     if "FETCH_SIZE" in avg:
         hbm = avg["FETCH_SIZE"] * 1024 * 2
         res["hbm_read_bytes_per_launch"] = int(hbm)
@@ -43,6 +47,10 @@ def main():
     px = alg / 2
     if "SQ_INSTS_VALU" in avg and "SQ_WAVES" in avg:
         res["valu_instr_per_pixel_per_lane"] = round(avg["SQ_INSTS_VALU"] * 64 / px, 2)
+    if "SQ_INSTS_SALU" in avg and "SQ_WAVES" in avg:
+        res["salu_instr_per_pixel_per_lane"] = round(avg["SQ_INSTS_SALU"] * 64 / px, 2)
+    if "SQ_WAVE_CYCLES" in avg and "SQ_WAVES" in avg:
+        res["waves"] = avg["SQ_WAVES"]
     if "SQ_LDS_BANK_CONFLICT" in avg and "SQ_LDS_IDX_ACTIVE" in avg:
         res["lds_bank_conflict_frac"] = round(avg["SQ_LDS_BANK_CONFLICT"] / max(avg["SQ_LDS_IDX_ACTIVE"], 1), 4)
     text = json.dumps(res, indent=1)

@@ -201,11 +201,30 @@ struct TableSet {
   hipEvent_t cost_ready = nullptr;  // the flagged_cost readback enqueued before it
   StreamUses users;                 // kernels that read the set
   uint64_t tick = 0;                // last use (LRU)
+  // AUTO's measured share per group: ChromaTables::flagged_words (the words
+  // the chroma-run kernel's exact path resolved) read back every few
+  // launches, over the words launched in between (Probe)
+  struct Probe {
+    uint64_t base = 0;          // the counter at the last landed readback
+    bool have_base = false;
+    uint64_t launched = 0;      // words launched on the chroma-run kernel since the last readback
+    uint64_t in_flight = 0;     // those of the readback in flight
+    double measured = -1.0;     // flagged words / words between the last two readbacks
+    int stripe_runs = 0;        // batches sent to the stripe kernel by the measured share
+  };
+  std::vector<Probe> probes;
+  unsigned long long* h_words = nullptr;  // pinned [groups_cap]: the readback
+  hipEvent_t words_ready = nullptr;
+  bool words_pending = false;
+  int chroma_runs = 0;  // AUTO chroma-run launches since the last readback
   void release() {
     users.wait_all();
     if (ready) (void)hipEventSynchronize(ready);
+    if (words_ready) (void)hipEventSynchronize(words_ready);
     users.release();
     (void)hipFree(d_chroma);
+    (void)hipHostFree(h_words);
+    if (words_ready) (void)hipEventDestroy(words_ready);
     (void)hipHostFree(h_cost);
     (void)hipFree(d_tables);
     (void)hipHostFree(h_tables);
@@ -458,6 +477,8 @@ int32_t acquire_tables(TrikCvHandle* h, const TRIK_VIDTRANSCODE_CV_InArgsAlg* ra
     HIP_TRY(hipMalloc(&v->d_stripe, sizeof(StripeTables) * groups));
     HIP_TRY(hipHostMalloc(&v->h_stripe, sizeof(StripeTables) * groups, hipHostMallocDefault));
     HIP_TRY(hipHostMalloc(&v->h_cost, sizeof(unsigned long long) * groups, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(&v->h_words, sizeof(unsigned long long) * groups, hipHostMallocDefault));
+    HIP_TRY(hipEventCreateWithFlags(&v->words_ready, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&v->ready, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&v->cost_ready, hipEventDisableTiming));
     v->groups_cap = groups;
@@ -478,6 +499,10 @@ int32_t acquire_tables(TrikCvHandle* h, const TRIK_VIDTRANSCODE_CV_InArgsAlg* ra
   v->key.swap(key);
   v->chroma_built = false;
   v->chroma_share = -1.0;
+  if (v->words_pending) (void)hipEventSynchronize(v->words_ready);
+  v->words_pending = false;
+  v->probes.assign(groups, TableSet::Probe());
+  v->chroma_runs = 0;
   v->tick = ++h->tick;
   *out = v;
   return 0;
@@ -507,7 +532,27 @@ int32_t ensure_chroma(TableSet& t, int groups, hipStream_t s) {
 // host, or GATED: both launched, the device picks by the builder's cost.
 enum HotPlan { kPlanStripe, kPlanChroma, kPlanGated };
 
-HotPlan plan_hot(TrikCvHandle* h, TableSet& t, int groups, bool big, bool chroma_ok, hipStream_t s,
+// Batches AUTO keeps on the stripe kernel for a group whose measured share
+// is too high before it tries the chroma-run kernel again (re-measuring), and
+// AUTO chroma-run launches between readbacks of the measured share.
+constexpr int kReprobeAfter = 32;
+constexpr int kProbeEvery = 8;
+
+// The measured shares, once their readback has landed (non-blocking).
+void poll_measured(TableSet& t) {
+  if (!t.words_pending || hipEventQuery(t.words_ready) != hipSuccess) return;
+  for (size_t g = 0; g < t.probes.size(); ++g) {
+    TableSet::Probe& p = t.probes[g];
+    const uint64_t v = t.h_words[g];
+    if (p.have_base && p.in_flight > 0) p.measured = (double)(v - p.base) / (double)p.in_flight;
+    p.base = v;
+    p.have_base = true;
+    p.in_flight = 0;
+  }
+  t.words_pending = false;
+}
+
+HotPlan plan_hot(TrikCvHandle* h, TableSet& t, int g, int groups, bool big, bool chroma_ok, hipStream_t s,
                  int32_t* rc) {
   *rc = 0;
   const int choice = h->hot.load();
@@ -517,7 +562,37 @@ HotPlan plan_hot(TrikCvHandle* h, TableSet& t, int groups, bool big, bool chroma
   if (choice == TRIK_HSV_HOT_CHROMA) return kPlanChroma;
   const double sh = t.share();
   if (sh < 0) return kPlanGated;  // the share is still in flight: no host wait
-  return sh <= TRIK_HSV_CHROMA_MAX_SHARE ? kPlanChroma : kPlanStripe;
+  if (sh > TRIK_HSV_CHROMA_MAX_SHARE) return kPlanStripe;
+  // the input's own share, measured on earlier batches: input that
+  // concentrates on the chromas the tables describe worst (their windows and
+  // exceptions) goes to the stripe kernel, with a chroma-run batch now and
+  // then to see whether it still does
+  TableSet::Probe& p = t.probes[g];
+  if (p.measured > TRIK_HSV_CHROMA_MAX_SHARE && ++p.stripe_runs <= kReprobeAfter) return kPlanStripe;
+  p.stripe_runs = 0;
+  return kPlanChroma;
+}
+
+// After a call's launches: AUTO chroma-run words counted, and every
+// kProbeEvery such launches (or right after a re-probe) the groups' exact-path
+// word counters read back into pinned memory without a host wait.
+int32_t probe_measured(TableSet& t, bool reprobe, hipStream_t s) {
+  if (t.chroma_runs == 0 || t.words_pending) return 0;
+  bool want = reprobe || t.chroma_runs >= kProbeEvery;
+  for (const TableSet::Probe& p : t.probes) want = want || !p.have_base;
+  if (!want) return 0;
+  const size_t n = t.probes.size();
+  for (size_t g = 0; g < n; ++g)
+    HIP_TRY(hipMemcpyAsync(&t.h_words[g], &t.d_chroma[g].flagged_words, sizeof(unsigned long long),
+                           hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipEventRecord(t.words_ready, s));
+  for (TableSet::Probe& p : t.probes) {
+    p.in_flight = p.launched;
+    p.launched = 0;
+  }
+  t.words_pending = true;
+  t.chroma_runs = 0;
+  return 0;
 }
 
 // The outputs of a full step (process_batch): sums written whole (not added),
@@ -560,6 +635,8 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
   std::vector<KernelArgs> args(empty ? 0 : groups);
   std::vector<HotPlan> plans(args.size(), kPlanStripe);
   bool fused = step != nullptr && !masks && !empty;
+  poll_measured(*t);
+  bool reprobe = false;
   for (size_t g = 0; g < args.size(); ++g) {
     KernelArgs& a = args[g];
     a.frames = static_cast<const uint8_t*>(b->frames);
@@ -581,9 +658,11 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
     // value-only groups (every range accepts every hue and saturation) run
     // the stripe kernel's value form under AUTO at any batch size: it beats
     // the chroma-run kernel there and needs no table build
-    plans[g] = plan_hot(h, *t, groups, big && t->detect[g] != kDetectV,
+    const bool was_measured_stripe = g < t->probes.size() && t->probes[g].stripe_runs > 0;
+    plans[g] = plan_hot(h, *t, (int)g, groups, big && t->detect[g] != kDetectV,
                         h->hot.load() != TRIK_HSV_HOT_GENERIC && chroma_geometry_ok(a), s, &rc);
     if (rc) return rc;
+    reprobe = reprobe || (was_measured_stripe && plans[g] == kPlanChroma);
     fused = fused && plans[g] == kPlanChroma && chroma_fused_ok(a);
   }
   if (fused) {
@@ -591,7 +670,7 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
     if (rc) return rc;
     HIP_TRY(h->fused_users.order_after(s));
   }
-  if (step && !fused && !empty && sums)
+  if (step && !fused && b->n_frames > 0 && sums)  // (frames of zero width or height: zero sums)
     HIP_TRY(hipMemsetAsync(sums, 0, sizeof(TrikHsvTargetSums) * (size_t)b->n_frames * n, s));
   bool gated = false;
   h->hot_groups.assign(groups, 0);
@@ -608,7 +687,13 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
         a.wg_cnt = h->d_wg_cnt;
       }
       e = launch_chroma(a, t->d_chroma + g, masks != nullptr, s);
-      if (e == hipSuccess) h->hot_groups[g] = TRIK_HSV_HOT_CHROMA;
+      if (e == hipSuccess) {
+        h->hot_groups[g] = TRIK_HSV_HOT_CHROMA;
+        if (h->hot.load() == TRIK_HSV_HOT_AUTO) {
+          t->probes[g].launched += (uint64_t)a.n_frames * (uint64_t)(a.width / 2) * (uint64_t)a.height;
+          if (g == 0) ++t->chroma_runs;
+        }
+      }
     } else if (plan == kPlanGated) {
       // AUTO's rule on the device: the chroma-run kernel runs while this
       // group's cost is at most kChromaMaxCost, its partner otherwise -- the
@@ -645,9 +730,13 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
     HIP_TRY(e);
   }
   h->pending_set = gated ? t : nullptr;
+  if (!masks) {
+    rc = probe_measured(*t, reprobe, s);
+    if (rc) return rc;
+  }
   if (step && !fused) {  // the epilogue and the totals as kernels of their own
-    if (step->targets && !empty) HIP_TRY(launch_targets(*b, n, sums, step->targets, s));
-    if (step->totals) HIP_TRY(launch_totals(empty ? 0 : b->n_frames, n, sums, step->totals, s));
+    if (step->targets) HIP_TRY(launch_targets(*b, n, sums, step->targets, s));
+    if (step->totals) HIP_TRY(launch_totals(b->n_frames > 0 ? b->n_frames : 0, n, sums, step->totals, s));
   }
   rc = t->users.note(s);
   if (!rc && fused) rc = h->fused_users.note(s);
@@ -850,7 +939,7 @@ int32_t blob_args(TrikCvHandle* h, const TrikHsvFrameBatch& b, const TRIK_VIDTRA
 int32_t run_blob(TrikCvHandle* h, BlobArgs& ba, TableSet& t, hipStream_t s) {
   const bool big = (int64_t)ba.n_frames * ba.width * ba.height >= (int64_t)TRIK_HSV_CHROMA_MIN_PIXELS;
   int32_t rc = 0;
-  const HotPlan plan = plan_hot(h, t, 1, big, h->hot.load() != TRIK_HSV_HOT_GENERIC && blob_chroma_ok(ba), s, &rc);
+  const HotPlan plan = plan_hot(h, t, 0, 1, big, h->hot.load() != TRIK_HSV_HOT_GENERIC && blob_chroma_ok(ba), s, &rc);
   if (rc) return rc;
   ba.meta_ready = 0;
   h->pending_set = nullptr;
@@ -1450,6 +1539,20 @@ extern "C" int32_t trik_hsv_chroma_share(TRIK_VIDTRANSCODE_CV_Handle h, double* 
     HIP_TRY(hipEventSynchronize(t->cost_ready));
     *share = t->share();
   }
+  return 0;
+}
+
+extern "C" int32_t trik_hsv_chroma_measured_share(TRIK_VIDTRANSCODE_CV_Handle h, double* share) {
+  if (!h || !share) return fail(TRIK_IVIDTRANSCODE_EFAIL, "NULL handle or share");
+  std::lock_guard<std::mutex> lock(h->mu);
+  DeviceGuard dg(h->device);
+  TableSet* t = h->sums_set;
+  *share = -1.0;
+  if (!t) return 0;
+  if (t->words_pending) HIP_TRY(hipEventSynchronize(t->words_ready));
+  poll_measured(*t);
+  for (const TableSet::Probe& p : t->probes)
+    if (p.measured > *share) *share = p.measured;
   return 0;
 }
 

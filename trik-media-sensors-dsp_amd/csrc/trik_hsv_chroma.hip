@@ -83,7 +83,10 @@ constexpr uint32_t kLdsRecMeta = kLdsRecWords + (kHotLanes / 64) * kRecCap * 16;
 constexpr uint32_t kFrameSlotBytes = 12 * 8 + 8;
 constexpr uint32_t kLdsFrames = (kLdsRecMeta + (kHotLanes / 64) * kRecCap * 4 + 7u) & ~7u;
 constexpr uint32_t kLdsTotals = kLdsFrames + kFrameSlots * kFrameSlotBytes;
-constexpr uint32_t kLdsBytes = kLdsTotals + 12 * 8 + 8;  // + the last-workgroup flag
+// + the last-workgroup flag; then the workgroup's exact-path word count and
+// its waves-done count
+constexpr uint32_t kLdsWords = kLdsTotals + 12 * 8 + 8;
+constexpr uint32_t kLdsBytes = kLdsWords + 8;
 static_assert(kLdsBytes <= 160 * 1024, "chroma kernel LDS image");
 static_assert((kRecCap * 16) % 16 == 0 && kRecCap >= 64 + 8, "record queue");
 
@@ -130,41 +133,31 @@ __device__ __forceinline__ void st64(uint32_t a, uint32_t x, uint32_t y) {
   *(lds64_t)(uintptr_t)a = v;
 }
 
-// The fast-path masks of the two pixels of YUYV word w under run descriptor
-// d = b1 | b2 << 8, block word bw (cut A in its byte 1) and mask pair (m1, m2): with lt = Y < b1,
-// le = Y <= b2, ge = Y >= A, e = le && ge ? (lt ? m1 : m2) : 0.  Byte operands
-// straight from w and d by SDWA compares; the selects follow all compares (the
-// VALU-writes-SGPR -> v_cndmask distance needs no nops).  q0 / q1 (wave masks,
-// SALU) flag the pixels the exact path resolves: a window pixel (lt and not
-// le, where the select gives 0; windows lie above the cut) or any pixel of an
-// exception-code word (le is cleared, so the select gives 0 as well).  vm
-// masks lanes without a valid row.
-#define TRIK_SELECT2_CMPS(AB)                                                                   \
+#define TRIK_SELECT2_CMPS                                                                       \
   "v_cmp_eq_u32_e64 %[x], %[k], %[d]\n\t"                                                       \
   "v_cmp_gt_u32_sdwa %[lt0], %[d], %[w] src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"                    \
   "v_cmp_gt_u32_sdwa %[lt1], %[d], %[w] src0_sel:BYTE_0 src1_sel:BYTE_2\n\t"                    \
   "v_cmp_ge_u32_sdwa %[le0], %[d], %[w] src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"                    \
   "v_cmp_ge_u32_sdwa %[le1], %[d], %[w] src0_sel:BYTE_1 src1_sel:BYTE_2\n\t"                    \
-  "v_cmp_le_u32_sdwa %[ge0], %[a], %[w] src0_sel:BYTE_" #AB " src1_sel:BYTE_0\n\t"              \
-  "v_cmp_le_u32_sdwa %[ge1], %[a], %[w] src0_sel:BYTE_" #AB " src1_sel:BYTE_2"
-// ABYTE: the byte of bw holding the cut A
-template <int ABYTE = 1>
-__device__ __forceinline__ void select2(uint32_t w, uint32_t d, uint32_t bw, uint32_t m1, uint32_t m2, uint64_t vm,
-                                        uint32_t& e0, uint32_t& e1, uint64_t& q0, uint64_t& q1) {
-  static_assert(ABYTE == 0 || ABYTE == 1, "cut byte");
+  "v_cmp_le_u32_sdwa %[ge0], %[a], %[w] src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"                    \
+  "v_cmp_le_u32_sdwa %[ge1], %[a], %[w] src0_sel:BYTE_1 src1_sel:BYTE_2"
+// The selects; q0 / q1 per pixel (MASKS) or only their union (the word is
+// flagged: one SALU op fewer per word).
+template <bool PER_PIXEL>
+__device__ __forceinline__ void select2_impl(uint32_t w, uint32_t d, uint32_t bw, uint32_t m1, uint32_t m2, uint64_t vm,
+                                             uint32_t& e0, uint32_t& e1, uint64_t& q0, uint64_t& q1) {
   uint64_t x, lt0, lt1, le0, le1, ge0, ge1;
-  if constexpr (ABYTE == 1)
-    asm volatile(TRIK_SELECT2_CMPS(1)
-                 : [x] "=&s"(x), [lt0] "=&s"(lt0), [lt1] "=&s"(lt1), [le0] "=&s"(le0), [le1] "=&s"(le1),
-                   [ge0] "=&s"(ge0), [ge1] "=&s"(ge1)
-                 : [w] "v"(w), [d] "v"(d), [a] "v"(bw), [k] "s"(kChromaExc));
-  else
-    asm volatile(TRIK_SELECT2_CMPS(0)
-                 : [x] "=&s"(x), [lt0] "=&s"(lt0), [lt1] "=&s"(lt1), [le0] "=&s"(le0), [le1] "=&s"(le1),
-                   [ge0] "=&s"(ge0), [ge1] "=&s"(ge1)
-                 : [w] "v"(w), [d] "v"(d), [a] "v"(bw), [k] "s"(kChromaExc));
-  q0 = (x | (lt0 & ~le0)) & vm;
-  q1 = (x | (lt1 & ~le1)) & vm;
+  asm volatile(TRIK_SELECT2_CMPS
+               : [x] "=&s"(x), [lt0] "=&s"(lt0), [lt1] "=&s"(lt1), [le0] "=&s"(le0), [le1] "=&s"(le1),
+                 [ge0] "=&s"(ge0), [ge1] "=&s"(ge1)
+               : [w] "v"(w), [d] "v"(d), [a] "v"(bw), [k] "s"(kChromaExc));
+  if (PER_PIXEL) {
+    q0 = (x | (lt0 & ~le0)) & vm;
+    q1 = (x | (lt1 & ~le1)) & vm;
+  } else {
+    q0 = (x | (lt0 & ~le0) | (lt1 & ~le1)) & vm;
+    q1 = 0;
+  }
   const uint64_t k0 = le0 & ge0 & ~x & vm, k1 = le1 & ge1 & ~x & vm;
   asm volatile(
       "v_cndmask_b32_e64 %[e0], %[m2], %[m1], %[lt0]\n\t"
@@ -173,6 +166,26 @@ __device__ __forceinline__ void select2(uint32_t w, uint32_t d, uint32_t bw, uin
       "v_cndmask_b32_e64 %[e1], 0, %[e1], %[k1]"
       : [e0] "=&v"(e0), [e1] "=&v"(e1)
       : [m1] "v"(m1), [m2] "v"(m2), [lt0] "s"(lt0), [lt1] "s"(lt1), [k0] "s"(k0), [k1] "s"(k1));
+}
+// The fast-path masks of the two pixels of YUYV word w under run descriptor
+// d = b1 | b2 << 8, block word bw (cut A in its byte 1) and mask pair (m1,
+// m2): with lt = Y < b1, le = Y <= b2, ge = Y >= A, e = le && ge ? (lt ? m1 :
+// m2) : 0.  Byte operands straight from w, d and bw by SDWA compares; the
+// selects follow all compares (the VALU-writes-SGPR -> v_cndmask distance
+// needs no nops).  q0 / q1 (wave masks, SALU) flag the pixels the exact path
+// resolves: a window pixel (lt and not le, where the select gives 0; windows
+// lie above the cut) or any pixel of an exception-code word (le is cleared,
+// so the select gives 0 as well).  vm masks lanes without a valid row.
+__device__ __forceinline__ void select2(uint32_t w, uint32_t d, uint32_t bw, uint32_t m1, uint32_t m2, uint64_t vm,
+                                        uint32_t& e0, uint32_t& e1, uint64_t& q0, uint64_t& q1) {
+  select2_impl<true>(w, d, bw, m1, m2, vm, e0, e1, q0, q1);
+}
+// The same, with only the word's flag (q0 | q1).
+__device__ __forceinline__ uint64_t select2w(uint32_t w, uint32_t d, uint32_t bw, uint32_t m1, uint32_t m2,
+                                             uint64_t vm, uint32_t& e0, uint32_t& e1) {
+  uint64_t q, unused;
+  select2_impl<false>(w, d, bw, m1, m2, vm, e0, e1, q, unused);
+  return q;
 }
 
 // Record store (a piece's 4 words at wa, its meta word at ma) by the lanes of
@@ -436,6 +449,7 @@ __global__ __launch_bounds__(1024) void chroma_cost_kernel(ChromaTables* ct) {
     unsigned long long sum = 0;
     for (int i = 0; i < 16; ++i) sum += part[i];
     ct->flagged_cost = sum;
+    ct->flagged_words = 0;
   }
 }
 
@@ -571,6 +585,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     }
     if (t < 12) st_u64(kLdsTotals + 8 * t, 0ull);
   }
+  if (t < 2) *(lds32_t)(uintptr_t)(kLdsWords + 4 * t) = 0u;
   __syncthreads();
 
   const int lane = t & 63;
@@ -599,6 +614,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
   const uint32_t meta_x = (x0 >> 3) << 4;
   const uint32_t meta_b = ((SPLIT ? dx >> 3 : 1u) << 4) + ((uint32_t)half << 16);
 
+  uint32_t resolved = 0;  // words this wave's exact path resolved (wave-uniform)
   // the frame and the tile within it, stepped along (wave-uniform, SALU)
   int fcur = __builtin_amdgcn_readfirstlane((int)(t_begin / g.tiles_per_frame));
   int trem = __builtin_amdgcn_readfirstlane((int)(t_begin - (int64_t)fcur * g.tiles_per_frame));
@@ -645,18 +661,15 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     // goes back to the queue with its remaining bits.  Verification mode
     // writes the exact masks.
     auto drain = [&](int take) {
+      resolved += (uint32_t)take;
       const uint32_t base = (uint32_t)(qn - take);
       const bool act = lane < take;
-      u32x4 w4 = {0u, 0u, 0u, 0u};
-      uint32_t meta = 0;
-      if (act) {
-        w4 = *(lds128_t)(uintptr_t)(rw_s + 16u * (base + (uint32_t)lane));
-        meta = *(lds32_t)(uintptr_t)(rm_s + 4u * (base + (uint32_t)lane));
-      }
+      const uint32_t rec = rw_s + 16u * (base + (uint32_t)lane);
+      const uint32_t meta = act ? *(lds32_t)(uintptr_t)(rm_s + 4u * (base + (uint32_t)lane)) : 0u;
       const uint32_t fl = meta & 15u;
       if (act) {
         const uint32_t i = (uint32_t)__builtin_ctz(fl);
-        const uint32_t w = (i & 2u) ? ((i & 1u) ? w4.w : w4.z) : ((i & 1u) ? w4.y : w4.x);
+        const uint32_t w = *(lds32_t)(uintptr_t)(rec + 4u * i);  // the record's first flagged word
         const uint32_t x = ((meta >> 4) & 0xFFFu) * 8u + 2u * i, yr = meta >> 16;
         const uint32_t d = ld16(kLdsRuns + 2u * chroma_of(w));
         const uint32_t lo = d & 0xFFu, hi = d >> 8, Y0 = w & 0xFFu, Y1 = (w >> 16) & 0xFFu;
@@ -683,7 +696,9 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
       // drained ones were (their reads above come first: LDS is in order)
       const uint32_t rest = fl & (fl - 1u);
       const uint64_t left = __builtin_amdgcn_ballot_w64(rest != 0u);
-      if (left) {
+      if (left) {  // (rare on camera-like and uniform input: a piece with two flagged words)
+        u32x4 w4 = {0u, 0u, 0u, 0u};
+        if (rest) w4 = *(lds128_t)(uintptr_t)rec;
         const uint32_t idx =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(left >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)left, base));
         store_record(left, rw_s + 16u * idx, w4, rm_s + 4u * idx, (meta & ~15u) | rest);
@@ -747,9 +762,13 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         uint64_t bal[CW];
 #pragma unroll
         for (int i = 0; i < CW; ++i) {
-          uint64_t q0, q1;
-          select2<1>(cw[i], d[i], cut[i], mm[i].x, mm[i].y, i < 4 ? vma : vmb, e[2 * i], e[2 * i + 1], q0, q1);
-          bal[i] = q0 | q1;
+          uint64_t q0 = 0, q1 = 0;
+          if (MASKS) {
+            select2(cw[i], d[i], cut[i], mm[i].x, mm[i].y, i < 4 ? vma : vmb, e[2 * i], e[2 * i + 1], q0, q1);
+            bal[i] = q0 | q1;
+          } else {
+            bal[i] = select2w(cw[i], d[i], cut[i], mm[i].x, mm[i].y, i < 4 ? vma : vmb, e[2 * i], e[2 * i + 1]);
+          }
           // formed here, so the word's compare masks die here (sunk into the
           // append branches they would all stay live in SGPRs)
           asm volatile("" : "+s"(bal[i]));
@@ -904,6 +923,16 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         *(lds32_t)(uintptr_t)(sb + 96) = 0u;
         st_release(sb + 100, (uint32_t)(f + kFrameSlots));
       }
+    }
+  }
+  // the exact-path word count: per workgroup in LDS, one device atomic by its
+  // last wave (AUTO's measured share, ChromaTables::flagged_words)
+  if (lane == 0) {
+    if (resolved) lds_add_rtn_u32(kLdsWords, resolved);
+    const uint32_t done = lds_add_rtn_u32(kLdsWords + 4, 1u);
+    if (done + 1 == (blockDim.x >> 6)) {
+      const uint32_t n = *(lds32_t)(uintptr_t)kLdsWords;
+      if (n) atomicAdd(const_cast<unsigned long long*>(&ct->flagged_words), (unsigned long long)n);
     }
   }
   // fused step: the per-target totals.  Every workgroup stores its totals; the

@@ -98,6 +98,10 @@ struct alignas(16) ChromaTables {
   // (chroma_cost): / 2^32 = the expected share of words the exact path takes
   // on uniform input; the host's AUTO selector reads it
   unsigned long long flagged_cost;
+  // words the hot kernel's exact path resolved, summed over its launches on
+  // these tables (zeroed by the build): the host's AUTO selector reads it back
+  // now and then to compare the input's actual share with flagged_cost's
+  unsigned long long flagged_words;
 };
 
 PackedRange pack_range(const TRIK_VIDTRANSCODE_CV_InArgsAlg& r);

@@ -186,6 +186,15 @@ class Detector(_HotKernel):
             raise TrikHsvError(rc, "trik_hsv_chroma_share")
         return v.value
 
+    def chroma_measured_share(self) -> float:
+        """The exact-path word share the chroma-run kernel measured on this
+        handle's recent AUTO batches of the current range set (-1 unknown)."""
+        v = C.c_double()
+        rc = _lib.trik_hsv_chroma_measured_share(self._h, C.byref(v))
+        if rc:
+            raise TrikHsvError(rc, "trik_hsv_chroma_measured_share")
+        return v.value
+
     def batch_masks(self, frames, width, height, line_length, layout, ranges, *, n_frames=None,
                     frame_stride=None, stream=None):
         """Verification mode: returns (masks uint8 [N,H,W], sums int64 [N,T,3])."""
