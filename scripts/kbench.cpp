@@ -36,6 +36,7 @@ struct Lib {
   void* so = nullptr;
   decltype(&TRIK_VIDTRANSCODE_CV_create) create;
   decltype(&trik_hsv_batch_sums) sums;
+  decltype(&trik_hsv_process_batch_totals) step = nullptr;
   decltype(&trik_hsv_synth) synth;
   decltype(&trik_hsv_set_hot_kernel) set_hot;
   decltype(&trik_hsv_last_error) last_error;
@@ -54,9 +55,9 @@ static void sym(void* so, const char* name, F& f) {
 }
 
 int main(int argc, char** argv) {
-  int frames = 4096, W = 640, H = 480, T = 4, kind = 0, iters = 20, rounds = 3, hot = 2, layout = 0;
+  int frames = 4096, W = 640, H = 480, T = 4, kind = 0, iters = 20, rounds = 3, hot = 2, layout = 0, full = 0;
   int opt;
-  while ((opt = getopt(argc, argv, "f:w:h:t:k:n:r:m:l:")) != -1) {
+  while ((opt = getopt(argc, argv, "f:w:h:t:k:n:r:m:l:s")) != -1) {
     switch (opt) {
       case 'f': frames = atoi(optarg); break;
       case 'w': W = atoi(optarg); break;
@@ -67,6 +68,7 @@ int main(int argc, char** argv) {
       case 'r': rounds = atoi(optarg); break;
       case 'm': hot = atoi(optarg); break;
       case 'l': layout = atoi(optarg); break;
+      case 's': full = 1; break;  // time the full step (trik_hsv_process_batch_totals)
       default: return 2;
     }
   }
@@ -81,6 +83,7 @@ int main(int argc, char** argv) {
     }
     sym(L.so, "TRIK_VIDTRANSCODE_CV_create", L.create);
     sym(L.so, "trik_hsv_batch_sums", L.sums);
+    if (full) sym(L.so, "trik_hsv_process_batch_totals", L.step);
     sym(L.so, "trik_hsv_synth", L.synth);
     sym(L.so, "trik_hsv_set_hot_kernel", L.set_hot);
     sym(L.so, "trik_hsv_last_error", L.last_error);
@@ -100,6 +103,10 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&d_sums, sb));
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  TrikHsvTarget* d_targets = nullptr;
+  TrikHsvTargetSums* d_totals = nullptr;
+  CK(hipMalloc(&d_targets, sizeof(TrikHsvTarget) * (size_t)frames * T));
+  CK(hipMalloc(&d_totals, sizeof(TrikHsvTargetSums) * T));
   TrikHsvFrameBatch b = {d_frames, fb, frames, W, H, ll, layout};
   if (libs[0].synth(&b, 0, kind, 0x7A1Cull, s)) {
     fprintf(stderr, "synth: %s\n", libs[0].last_error());
@@ -111,7 +118,7 @@ int main(int argc, char** argv) {
     if (L.create(nullptr, &L.h)) return 2;
     L.set_hot(L.h, hot);
     CK(hipMemsetAsync(d_sums, 0, sb, s));
-    if (L.sums(L.h, &b, all, T, d_sums, s)) {
+    if ((full ? L.step(L.h, &b, all, T, d_sums, d_targets, d_totals, s) : L.sums(L.h, &b, all, T, d_sums, s))) {
       fprintf(stderr, "%s: %s\n", L.path.c_str(), L.last_error());
       return 2;
     }
@@ -129,10 +136,10 @@ int main(int argc, char** argv) {
   for (int r = 0; r < rounds; ++r)
     for (Lib& L : libs) {
       L.set_hot(L.h, hot);
-      for (int w = 0; w < 3; ++w) L.sums(L.h, &b, all, T, d_sums, s);
+      for (int w = 0; w < 3; ++w) (full ? L.step(L.h, &b, all, T, d_sums, d_targets, d_totals, s) : L.sums(L.h, &b, all, T, d_sums, s));
       for (int k = 0; k < iters; ++k) {
         CK(hipEventRecord(e0, s));
-        L.sums(L.h, &b, all, T, d_sums, s);
+        (full ? L.step(L.h, &b, all, T, d_sums, d_targets, d_totals, s) : L.sums(L.h, &b, all, T, d_sums, s));
         CK(hipEventRecord(e1, s));
         CK(hipEventSynchronize(e1));
         float ms = 0;

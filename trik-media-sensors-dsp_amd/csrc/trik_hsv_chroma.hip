@@ -615,6 +615,8 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
   const uint32_t meta_b = ((SPLIT ? dx >> 3 : 1u) << 4) + ((uint32_t)half << 16);
 
   uint32_t resolved = 0;  // words this wave's exact path resolved (wave-uniform)
+  // fused step: the arrivals that complete a frame (every wave, every tile of it)
+  const uint32_t frame_arrivals = __builtin_amdgcn_readfirstlane((blockDim.x >> 6) * (uint32_t)g.tiles_per_frame);
   // the frame and the tile within it, stepped along (wave-uniform, SALU)
   int fcur = __builtin_amdgcn_readfirstlane((int)(t_begin / g.tiles_per_frame));
   int trem = __builtin_amdgcn_readfirstlane((int)(t_begin - (int64_t)fcur * g.tiles_per_frame));
@@ -839,6 +841,9 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         if (FULL) return rb + hb + voff;
         return s < vstepsb ? pf + hb + (int64_t)s * rowstep : pf;
       };
+      // (the load past the tile's last step re-reads its last rows: an
+      // unconditional load keeps the step's wait at "this step's data"; a
+      // branch around it makes the compiler wait for every load in flight)
       uint32_t wa[CW], wb[CW];
       load_chunk<LAYOUT>(row_ptr(0), row_ptr_b(0), plane, wa);
       for (int s = 0; s < steps; s += 2) {
@@ -896,8 +901,10 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
       continue;
     }
     // fused step: the wave's values go into the frame's LDS slot; the last
-    // wave to finish the frame's last tile stores its sums and targets and
-    // adds them to the workgroup's totals, then frees the slot for frame + 4
+    // wave to finish the frame's last tile stores its sums and adds them to
+    // the workgroup's totals, then frees the slot for frame + 4 (the targets
+    // wait for the workgroup's end: their divisions would make the frame's
+    // last wave, already the slowest, slower still)
     const uint32_t sb = kLdsFrames + (uint32_t)((f - f_first) & (kFrameSlots - 1)) * kFrameSlotBytes;
     while (__builtin_amdgcn_readfirstlane(ld_acquire(sb + 100)) != (uint32_t)f) __builtin_amdgcn_s_sleep(2);
     if ((lane & 15) == 15 && rr < NR) {
@@ -907,7 +914,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     uint32_t arrived = 0;
     if (lane == 0) arrived = lds_add_rtn_u32(sb + 96, 1u);  // after this wave's adds (LDS is in order)
     arrived = __builtin_amdgcn_readfirstlane(arrived);
-    if (arrived + 1 == (blockDim.x >> 6) * (uint32_t)g.tiles_per_frame) {
+    if (arrived + 1 == frame_arrivals) {
       const int64_t o = (int64_t)f * a.sums_ranges + a.range_offset;
       const bool mine = lane < 3 * NR;
       const unsigned long long v = mine ? ld_u64(sb + 8u * (uint32_t)lane) : 0ull;
@@ -915,9 +922,6 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         reinterpret_cast<unsigned long long*>(&a.sums[o + lane / 3].points)[lane % 3] = v;
         lds_add_u64(kLdsTotals + 8u * (uint32_t)lane, v);
       }
-      if (a.targets && lane < NR)
-        a.targets[o + lane] = target_of(ld_u64(sb + 24u * (uint32_t)lane), ld_u64(sb + 24u * (uint32_t)lane + 8u),
-                                        ld_u64(sb + 24u * (uint32_t)lane + 16u), a.width, a.height);
       if (lane < 12) st_u64(sb + 8u * (uint32_t)lane, 0ull);
       if (lane == 0) {
         *(lds32_t)(uintptr_t)(sb + 96) = 0u;
@@ -935,23 +939,38 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
       if (n) atomicAdd(const_cast<unsigned long long*>(&ct->flagged_words), (unsigned long long)n);
     }
   }
+  if (!a.fused) return;
+  __syncthreads();  // (workgroup scope: this workgroup's sums stores are visible to it)
+  // fused step: the targets of this workgroup's frames, from the sums it stored
+  if (a.targets) {
+    const int64_t f_end = (int64_t)a.n_frames * (blockIdx.x + 1) / gridDim.x;
+    for (int64_t i = t; i < (f_end - f_first) * NR; i += blockDim.x) {
+      const int64_t o = (f_first + i / NR) * a.sums_ranges + a.range_offset + i % NR;
+      const TrikHsvTargetSums sm = a.sums[o];
+      a.targets[o] = target_of((uint64_t)sm.points, (uint64_t)sm.sum_x, (uint64_t)sm.sum_y, a.width, a.height);
+    }
+  }
   // fused step: the per-target totals.  Every workgroup stores its totals; the
   // last one to finish (a device-scope counter, reset by it for the next
   // launch) sums them into a.totals.
-  if (!a.fused || !a.totals) return;
-  __syncthreads();
-  unsigned long long* part = a.wg_part + 12 * (int64_t)blockIdx.x;
-  if (t < 12) part[t] = ld_u64(kLdsTotals + 8u * (uint32_t)t);
-  __threadfence();
-  __syncthreads();
-  if (t == 0) {
-    const uint32_t done = atomicAdd(a.wg_cnt, 1u);
-    *(lds32_t)(uintptr_t)(kLdsTotals + 96) = done + 1 == gridDim.x ? 1u : 0u;
+  if (!a.totals) return;
+  // wave 0 alone publishes (its 12 stores, one device-scope fence: an L2
+  // write-back per workgroup, not per wave) and counts the workgroup done
+  if (t < 64) {
+    unsigned long long* part = a.wg_part + 12 * (int64_t)blockIdx.x;
+    if (t < 12) {
+      part[t] = ld_u64(kLdsTotals + 8u * (uint32_t)t);
+      st_u64(kLdsTotals + 8u * (uint32_t)t, 0ull);
+    }
+    __threadfence();
+    if (t == 0) {
+      const uint32_t done = atomicAdd(a.wg_cnt, 1u);
+      *(lds32_t)(uintptr_t)(kLdsTotals + 96) = done + 1 == gridDim.x ? 1u : 0u;
+      if (done + 1 == gridDim.x) __threadfence();  // the last one: acquire the others' totals
+    }
   }
-  if (t < 12) st_u64(kLdsTotals + 8u * (uint32_t)t, 0ull);
   __syncthreads();
   if (*(lds32_t)(uintptr_t)(kLdsTotals + 96) == 0u) return;
-  __threadfence();
   for (uint32_t j = (uint32_t)t; j < 12u * gridDim.x; j += blockDim.x)
     lds_add_u64(kLdsTotals + 8u * (j % 12u),
                 __hip_atomic_load(a.wg_part + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));

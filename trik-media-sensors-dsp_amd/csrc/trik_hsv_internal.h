@@ -158,8 +158,11 @@ __device__ __forceinline__ TrikHsvTarget target_of(uint64_t points, uint64_t sum
                                                    int height) {
   TrikHsvTarget r = {0, 0, 0, 0};
   if (points > 0) {
-    const int32_t cx = (int32_t)(sum_x / points);
-    const int32_t cy = (int32_t)(sum_y / points);
+    // 32-bit divisions whenever the sums fit (every frame of the reference's
+    // sizes), 64-bit ones beyond
+    const bool narrow = ((sum_x | sum_y | points) >> 32) == 0;
+    const int32_t cx = (int32_t)(narrow ? (uint32_t)sum_x / (uint32_t)points : sum_x / points);
+    const int32_t cy = (int32_t)(narrow ? (uint32_t)sum_y / (uint32_t)points : sum_y / points);
     const float q = __fdiv_rn((float)(uint32_t)points, 3.1415927f);
     const uint32_t radius = (uint32_t)ceilf(__fsqrt_rn(q));  // WSEQ:492
     r.x = (int8_t)(((cx - width / 2) * 100 * 2) / width);   // WSEQ:496-498
