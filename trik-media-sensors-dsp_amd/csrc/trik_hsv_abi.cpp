@@ -619,7 +619,7 @@ int32_t ensure_fused_scratch(TrikCvHandle* h, hipStream_t s) {
 // Without `step` the kernels ADD into sums (the caller zeroes it).  With it
 // the call is a full step: when every group runs the chroma-run kernel and the
 // batch gives each workgroup whole frames (chroma_fused_ok), each launch
-// stores its sums and writes its targets and totals itself (the fused step,
+// zeroes its sums and writes its targets and totals itself (the fused step,
 // one launch per group); otherwise sums are zeroed first and the epilogue and
 // totals kernels follow.
 int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,

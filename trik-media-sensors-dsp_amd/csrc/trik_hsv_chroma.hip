@@ -57,8 +57,6 @@ constexpr int kQueueCap = 128;  // blob kernel, entries per wave: < 64 waiting +
 // LDS image leaves; a step starts with < 64 records queued.
 constexpr int kHotLanes = 960;
 constexpr int kRecCap = 73;
-// fused step: frames in flight per workgroup (a ring of LDS accumulators)
-constexpr int kFrameSlots = 4;
 
 // LDS image of the chroma kernel (dynamic LDS from address 0).  The block
 // masks and the mask-pair table sit below 64 KiB so their reads take an
@@ -78,15 +76,14 @@ static_assert(kLdsBlocks + 8192 <= kLdsPairs, "LDS layout");
 // x / 8 (bits 4-15) | row in the tile (bits 16-31)
 constexpr uint32_t kLdsRecWords = kLdsQueues;
 constexpr uint32_t kLdsRecMeta = kLdsRecWords + (kHotLanes / 64) * kRecCap * 16;
-// fused step: per frame slot 12 u64 sums (3 per range), the waves' arrival
-// count and the frame the slot takes (tag); then the workgroup's 12 u64 totals
-constexpr uint32_t kFrameSlotBytes = 12 * 8 + 8;
-constexpr uint32_t kLdsFrames = (kLdsRecMeta + (kHotLanes / 64) * kRecCap * 4 + 7u) & ~7u;
-constexpr uint32_t kLdsTotals = kLdsFrames + kFrameSlots * kFrameSlotBytes;
+// fused step: the workgroup's 12 u64 totals (3 per range)
+constexpr uint32_t kLdsTotals = (kLdsRecMeta + (kHotLanes / 64) * kRecCap * 4 + 7u) & ~7u;
 // + the last-workgroup flag; then the workgroup's exact-path word count and
 // its waves-done count
 constexpr uint32_t kLdsWords = kLdsTotals + 12 * 8 + 8;
-constexpr uint32_t kLdsBytes = kLdsWords + 8;
+// + the workgroup's unit counter (hot kernel: units handed out to waves)
+constexpr uint32_t kLdsUnits = kLdsWords + 8;
+constexpr uint32_t kLdsBytes = kLdsUnits + 4;
 static_assert(kLdsBytes <= 160 * 1024, "chroma kernel LDS image");
 static_assert((kRecCap * 16) % 16 == 0 && kRecCap >= 64 + 8, "record queue");
 
@@ -106,21 +103,11 @@ __device__ __forceinline__ unsigned long long ld_u64(uint32_t a) {
 __device__ __forceinline__ void st_u64(uint32_t a, unsigned long long v) {
   *(__attribute__((address_space(3))) unsigned long long*)(uintptr_t)a = v;
 }
-// the fused step's frame-slot tags: acquire loads, release stores (the slot's
-// sums are zeroed before its tag moves on)
-__device__ __forceinline__ uint32_t ld_acquire(uint32_t a) {
-  return __hip_atomic_load((__attribute__((address_space(3))) uint32_t*)(uintptr_t)a, __ATOMIC_ACQUIRE,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void st_release(uint32_t a, uint32_t v) {
-  __hip_atomic_store((__attribute__((address_space(3))) uint32_t*)(uintptr_t)a, v, __ATOMIC_RELEASE,
-                     __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 __device__ __forceinline__ void lds_add_u64(uint32_t a, unsigned long long v) {
   __hip_atomic_fetch_add((__attribute__((address_space(3))) unsigned long long*)(uintptr_t)a, v, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// a frame slot's arrival count: acq_rel, so a wave's sums are added before it
+// the workgroup's done counts: acq_rel, so a wave's adds come before it
 // counts itself and the last wave reads them after
 __device__ __forceinline__ uint32_t lds_add_rtn_u32(uint32_t a, uint32_t v) {
   return __hip_atomic_fetch_add((__attribute__((address_space(3))) uint32_t*)(uintptr_t)a, v, __ATOMIC_ACQ_REL,
@@ -572,29 +559,25 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     }
   }
   // fused step: this workgroup's frames [f_first, f_end) (whole frames), its
-  // tiles; the frame slots' sums zeroed and tagged with their first frames
+  // tiles; their sums zeroed here (no other workgroup adds to them: the
+  // stores reach L2 before this workgroup's first atomic, see the wait)
   const int64_t f_first = a.fused ? (int64_t)a.n_frames * blockIdx.x / gridDim.x : 0;
+  const int64_t f_end = a.fused ? (int64_t)a.n_frames * (blockIdx.x + 1) / gridDim.x : 0;
   const int64_t t_begin = a.fused ? f_first * g.tiles_per_frame : g.n_tiles * blockIdx.x / gridDim.x;
-  const int64_t t_end = a.fused ? (int64_t)a.n_frames * (blockIdx.x + 1) / gridDim.x * g.tiles_per_frame
-                                : g.n_tiles * (blockIdx.x + 1) / gridDim.x;
+  const int64_t t_end = a.fused ? f_end * g.tiles_per_frame : g.n_tiles * (blockIdx.x + 1) / gridDim.x;
   if (a.fused) {
-    if (t < kFrameSlots * 12) st_u64(kLdsFrames + (t / 12) * kFrameSlotBytes + 8 * (t % 12), 0ull);
-    if (t < kFrameSlots) {
-      *(lds32_t)(uintptr_t)(kLdsFrames + t * kFrameSlotBytes + 96) = 0u;
-      *(lds32_t)(uintptr_t)(kLdsFrames + t * kFrameSlotBytes + 100) = (uint32_t)(f_first + t);
-    }
+    for (int64_t i = t; i < (f_end - f_first) * NR; i += blockDim.x)
+      a.sums[(f_first + i / NR) * a.sums_ranges + a.range_offset + i % NR] = TrikHsvTargetSums{0, 0, 0};
     if (t < 12) st_u64(kLdsTotals + 8 * t, 0ull);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  if (t < 2) *(lds32_t)(uintptr_t)(kLdsWords + 4 * t) = 0u;
+  if (t < 3) *(lds32_t)(uintptr_t)(kLdsWords + 4 * t) = 0u;
   __syncthreads();
 
   const int lane = t & 63;
   const uint32_t wave = (uint32_t)(t >> 6);
   const uint32_t rw_s = __builtin_amdgcn_readfirstlane(kLdsRecWords + wave * (kRecCap * 16u));
   const uint32_t rm_s = __builtin_amdgcn_readfirstlane(kLdsRecMeta + wave * (kRecCap * 4u));
-  const bool active = t < g.k * g.cpr;
-  const int col = active ? t % g.cpr : 0;
-  const int ro = active ? t / g.cpr : 0;
   // YUYV: a lane's 8 words are 4 from row y (piece a) and 4 from row y + dy,
   // dx pixels right (piece b; word i at x0 + 2 (i & 3)); ov7670: 8 words of
   // row y (piece b 8 pixels right; word i at x0 + 2i)
@@ -605,30 +588,37 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
   const uint32_t dx = SPLIT ? (uint32_t)g.dx : 0u;  // and pixels
   const int64_t hb = (int64_t)half * a.line_length + 2 * (int64_t)dx;
   constexpr int kQBlock = 5;  // Q block: CW * n * (n + 1) <= 255
-  const int col_bytes = LAYOUT == TRIK_HSV_LAYOUT_YUYV ? col * 16 : col * 2 * CW;
-  const uint32_t x0 = (uint32_t)col * (SPLIT ? 8u : 2u * CW);
-  const uint32_t voff = (uint32_t)ro * (uint32_t)a.line_length + (uint32_t)col_bytes;
   auto xoff = [=](int i) { return SPLIT ? (i < 4 ? 0u : dx) + 2u * (uint32_t)(i & 3) : 2u * (uint32_t)i; };
-  // a record's meta word without its flag bits: x / 8 of the piece's first
-  // pixel and its row in the tile (piece b: xb8 * 8 pixels right, half rows down)
-  const uint32_t meta_x = (x0 >> 3) << 4;
   const uint32_t meta_b = ((SPLIT ? dx >> 3 : 1u) << 4) + ((uint32_t)half << 16);
 
   uint32_t resolved = 0;  // words this wave's exact path resolved (wave-uniform)
-  // fused step: the arrivals that complete a frame (every wave, every tile of it)
-  const uint32_t frame_arrivals = __builtin_amdgcn_readfirstlane((blockDim.x >> 6) * (uint32_t)g.tiles_per_frame);
-  // the frame and the tile within it, stepped along (wave-uniform, SALU)
-  int fcur = __builtin_amdgcn_readfirstlane((int)(t_begin / g.tiles_per_frame));
-  int trem = __builtin_amdgcn_readfirstlane((int)(t_begin - (int64_t)fcur * g.tiles_per_frame));
-  for (int64_t tile = t_begin; tile < t_end; ++tile) {
+  // Units: a tile's lanes in wave-sized groups (unit u: tile u / U, lanes
+  // 64 (u % U) ..), handed to the waves in order as they finish (a wave's
+  // first unit is its own index): the waves of a SIMD with fewer waves run
+  // faster and take more units, so the SIMDs end together.
+  const uint32_t U = blockDim.x >> 6;
+  const uint32_t n_units = (uint32_t)(t_end - t_begin) * U;
+  for (uint32_t u = wave; u < n_units;) {
+    uint32_t next = 0;
+    if (lane == 0) next = __hip_atomic_fetch_add((__attribute__((address_space(3))) uint32_t*)(uintptr_t)kLdsUnits,
+                                                 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t tl = u / U;
+    const int64_t tile = t_begin + tl;
+    const int f = (int)(tile / g.tiles_per_frame);
+    const int trem = (int)(tile - (int64_t)f * g.tiles_per_frame);
+    const int lt = (int)((u - tl * U) * 64u) + lane;  // the lane's index in the tile
+    const bool active = lt < g.k * g.cpr;
+    const int col = active ? lt % g.cpr : 0;
+    const int ro = active ? lt / g.cpr : 0;
+    const int col_bytes = LAYOUT == TRIK_HSV_LAYOUT_YUYV ? col * 16 : col * 2 * CW;
+    const uint32_t x0 = (uint32_t)col * (SPLIT ? 8u : 2u * CW);
+    const uint32_t voff = (uint32_t)ro * (uint32_t)a.line_length + (uint32_t)col_bytes;
+    // a record's meta word without its flag bits: x / 8 of the piece's first
+    // pixel and its row in the tile (piece b: xb8 * 8 pixels right, half rows down)
+    const uint32_t meta_x = (x0 >> 3) << 4;
     const int r0 = trem * g.rstep * g.steps;
     const int y0 = r0 + ro;
     const int steps = trem == g.tiles_per_frame - 1 ? g.steps_last : g.steps;
-    const int f = fcur;
-    if (++trem == g.tiles_per_frame) {
-      trem = 0;
-      ++fcur;
-    }
     const uint8_t* p = a.frames + (int64_t)f * a.frame_stride + (int64_t)y0 * a.line_length + col_bytes;
 
     uint32_t P[CW], O = 0, Q = 0, CumS = 0, CumA = 0, CumB = 0;
@@ -890,44 +880,19 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     wave_sums12(red);
     // lane 16 r + 15 holds values 3 r .. 3 r + 2: range r's N, sum x, sum y
     const int rr = lane >> 4;
-    if (!a.fused) {
-      if ((lane & 15) == 15 && rr < NR) {
-        unsigned long long* dst =
-            reinterpret_cast<unsigned long long*>(&a.sums[(int64_t)f * a.sums_ranges + a.range_offset + rr].points);
-#pragma unroll
-        for (int v = 0; v < 3; ++v)
-          if (red[v]) atomicAdd(dst + v, (unsigned long long)red[v]);
-      }
-      continue;
-    }
-    // fused step: the wave's values go into the frame's LDS slot; the last
-    // wave to finish the frame's last tile stores its sums and adds them to
-    // the workgroup's totals, then frees the slot for frame + 4 (the targets
-    // wait for the workgroup's end: their divisions would make the frame's
-    // last wave, already the slowest, slower still)
-    const uint32_t sb = kLdsFrames + (uint32_t)((f - f_first) & (kFrameSlots - 1)) * kFrameSlotBytes;
-    while (__builtin_amdgcn_readfirstlane(ld_acquire(sb + 100)) != (uint32_t)f) __builtin_amdgcn_s_sleep(2);
+    // the frame's sums: device atomics (fire and forget: no wave waits for
+    // another); fused step: the workgroup's totals in LDS
     if ((lane & 15) == 15 && rr < NR) {
+      unsigned long long* dst =
+          reinterpret_cast<unsigned long long*>(&a.sums[(int64_t)f * a.sums_ranges + a.range_offset + rr].points);
 #pragma unroll
-      for (int v = 0; v < 3; ++v) lds_add_u64(sb + 8u * (uint32_t)(3 * rr + v), red[v]);
+      for (int v = 0; v < 3; ++v)
+        if (red[v]) {
+          atomicAdd(dst + v, (unsigned long long)red[v]);
+          if (a.fused) lds_add_u64(kLdsTotals + 8u * (uint32_t)(3 * rr + v), red[v]);
+        }
     }
-    uint32_t arrived = 0;
-    if (lane == 0) arrived = lds_add_rtn_u32(sb + 96, 1u);  // after this wave's adds (LDS is in order)
-    arrived = __builtin_amdgcn_readfirstlane(arrived);
-    if (arrived + 1 == frame_arrivals) {
-      const int64_t o = (int64_t)f * a.sums_ranges + a.range_offset;
-      const bool mine = lane < 3 * NR;
-      const unsigned long long v = mine ? ld_u64(sb + 8u * (uint32_t)lane) : 0ull;
-      if (mine) {
-        reinterpret_cast<unsigned long long*>(&a.sums[o + lane / 3].points)[lane % 3] = v;
-        lds_add_u64(kLdsTotals + 8u * (uint32_t)lane, v);
-      }
-      if (lane < 12) st_u64(sb + 8u * (uint32_t)lane, 0ull);
-      if (lane == 0) {
-        *(lds32_t)(uintptr_t)(sb + 96) = 0u;
-        st_release(sb + 100, (uint32_t)(f + kFrameSlots));
-      }
-    }
+    u = __builtin_amdgcn_readfirstlane(next) + U;
   }
   // the exact-path word count: per workgroup in LDS, one device atomic by its
   // last wave (AUTO's measured share, ChromaTables::flagged_words)
@@ -940,14 +905,19 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     }
   }
   if (!a.fused) return;
-  __syncthreads();  // (workgroup scope: this workgroup's sums stores are visible to it)
-  // fused step: the targets of this workgroup's frames, from the sums it stored
+  // every wave's sums atomics performed at L2 before the workgroup reads them
+  // back (with L2 loads: this CU's L1 never saw them)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // fused step: the targets of this workgroup's frames, from their sums
   if (a.targets) {
-    const int64_t f_end = (int64_t)a.n_frames * (blockIdx.x + 1) / gridDim.x;
     for (int64_t i = t; i < (f_end - f_first) * NR; i += blockDim.x) {
       const int64_t o = (f_first + i / NR) * a.sums_ranges + a.range_offset + i % NR;
-      const TrikHsvTargetSums sm = a.sums[o];
-      a.targets[o] = target_of((uint64_t)sm.points, (uint64_t)sm.sum_x, (uint64_t)sm.sum_y, a.width, a.height);
+      unsigned long long* sp = reinterpret_cast<unsigned long long*>(&a.sums[o].points);
+      const uint64_t n = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t sx = __hip_atomic_load(sp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t sy = __hip_atomic_load(sp + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      a.targets[o] = target_of(n, sx, sy, a.width, a.height);
     }
   }
   // fused step: the per-target totals.  Every workgroup stores its totals; the

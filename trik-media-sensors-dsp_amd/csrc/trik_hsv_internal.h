@@ -138,10 +138,10 @@ struct KernelArgs {
   unsigned long long gate_max = 0;
   int32_t gate_le = 0;
   // The fused step (chroma-run kernel; chroma_fused_ok): whole frames per
-  // workgroup, so a frame's sums are complete inside one workgroup and are
-  // stored, not added (no zeroing); the same launch writes the targets and
-  // the per-target batch totals (the last workgroup sums the workgroups'
-  // partial totals).  DESIGN.md section 4.5.
+  // workgroup, so a frame's sums are zeroed, added and read back inside one
+  // workgroup (no memset launch); the same launch writes the targets and the
+  // per-target batch totals (the last workgroup sums the workgroups' partial
+  // totals).  DESIGN.md section 4.5.
   int32_t fused = 0;
   TrikHsvTarget* targets = nullptr;       // [n_frames][sums_ranges], or NULL
   TrikHsvTargetSums* totals = nullptr;    // [sums_ranges], or NULL
