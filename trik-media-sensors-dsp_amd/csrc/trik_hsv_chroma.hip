@@ -598,14 +598,16 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
   // faster and take more units, so the SIMDs end together.
   const uint32_t U = blockDim.x >> 6;
   const uint32_t n_units = (uint32_t)(t_end - t_begin) * U;
-  for (uint32_t u = wave; u < n_units;) {
+  for (uint32_t u = __builtin_amdgcn_readfirstlane(wave); u < n_units;) {  // (wave-uniform: SGPRs)
     uint32_t next = 0;
     if (lane == 0) next = __hip_atomic_fetch_add((__attribute__((address_space(3))) uint32_t*)(uintptr_t)kLdsUnits,
                                                  1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const uint32_t tl = u / U;
+    // (the divisions run on the VALU: their wave-uniform results are moved to
+    // SGPRs, else everything derived from them stays in VGPRs)
+    const uint32_t tl = __builtin_amdgcn_readfirstlane(u / U);
     const int64_t tile = t_begin + tl;
-    const int f = (int)(tile / g.tiles_per_frame);
-    const int trem = (int)(tile - (int64_t)f * g.tiles_per_frame);
+    const int f = __builtin_amdgcn_readfirstlane((int)(tile / g.tiles_per_frame));
+    const int trem = __builtin_amdgcn_readfirstlane((int)(tile - (int64_t)f * g.tiles_per_frame));
     const int lt = (int)((u - tl * U) * 64u) + lane;  // the lane's index in the tile
     const bool active = lt < g.k * g.cpr;
     const int col = active ? lt % g.cpr : 0;
@@ -629,22 +631,37 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     // record queue (wave-uniform count) and this lane's exact-path sums
     int qn = 0;
     ExcSums ex;
-    uint32_t xacc[3 * NR];
-#pragma unroll
-    for (int v = 0; v < 3 * NR; ++v) xacc[v] = 0;
-
-    auto unpack_exc = [&]() {
+    // the exact-path sums unpacked into 12 per-lane values (then zeroed)
+    auto unpack_exc = [&](uint32_t (&v)[12]) {
 #pragma unroll
       for (int rr = 0; rr < NR; ++rr) {
         const uint32_t sx = (rr & 1) ? ex.SX13 : ex.SX02, sy = (rr & 1) ? ex.SY13 : ex.SY02;
         const int sh = (rr >> 1) * 16;
         const uint32_t n = (ex.EN >> (8 * rr)) & 0xFFu;
-        xacc[3 * rr + 0] += n;
-        xacc[3 * rr + 1] += (sx >> sh) & 0xFFFFu;
-        xacc[3 * rr + 2] += ((sy >> sh) & 0xFFFFu) + (uint32_t)r0 * n;
+        v[3 * rr + 0] += n;
+        v[3 * rr + 1] += (sx >> sh) & 0xFFFFu;
+        v[3 * rr + 2] += ((sy >> sh) & 0xFFFFu) + (uint32_t)r0 * n;
       }
       ex.EN = ex.SX02 = ex.SX13 = ex.SY02 = ex.SY13 = 0;
       ex.rounds = 0;
+    };
+    // 12 per-lane values summed over the wave into the frame's sums: device
+    // atomics (fire and forget: no wave waits for another); fused step: the
+    // workgroup's totals in LDS
+    auto emit = [&](uint32_t (&v)[12]) {
+      wave_sums12(v);
+      // lane 16 r + 15 holds values 3 r .. 3 r + 2: range r's N, sum x, sum y
+      const int rr = lane >> 4;
+      if ((lane & 15) == 15 && rr < NR) {
+        unsigned long long* dst =
+            reinterpret_cast<unsigned long long*>(&a.sums[(int64_t)f * a.sums_ranges + a.range_offset + rr].points);
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          if (v[j]) {
+            atomicAdd(dst + j, (unsigned long long)v[j]);
+            if (a.fused) lds_add_u64(kLdsTotals + 8u * (uint32_t)(3 * rr + j), v[j]);
+          }
+      }
     };
     // One drain round: lanes 0..take-1 take the last take records, resolve
     // the first flagged word of each exactly (which of its pixels the fast
@@ -683,7 +700,11 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         ex.SY02 += (a0 + a1) * yr;
         ex.SY13 += (b0 + b1) * yr;
       }
-      if (++ex.rounds == g.flush_rounds) unpack_exc();
+      if (++ex.rounds == g.flush_rounds) {  // (rare: the 16-bit sums would overflow)
+        uint32_t v[12] = {};
+        unpack_exc(v);
+        emit(v);
+      }
       // records with flagged words left go back, compacted, where the
       // drained ones were (their reads above come first: LDS is in order)
       const uint32_t rest = fl & (fl - 1u);
@@ -821,39 +842,37 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
           nb = 0;
         }
       };
-      // rows of step s + 1 loaded while step s is processed
-      const uint8_t* rb = tbase;
-      auto row_ptr = [&](int s) -> const uint8_t* {
-        if (FULL) return rb + voff;
-        return s < vsteps ? pf + (int64_t)s * rowstep : pf;
-      };
-      auto row_ptr_b = [&](int s) -> const uint8_t* {
-        if (FULL) return rb + hb + voff;
-        return s < vstepsb ? pf + hb + (int64_t)s * rowstep : pf;
-      };
+      // rows of step s + 1 loaded while step s is processed (a third buffer,
+      // two steps ahead, measured no faster: the kernel is VALU-bound)
       // (the load past the tile's last step re-reads its last rows: an
       // unconditional load keeps the step's wait at "this step's data"; a
       // branch around it makes the compiler wait for every load in flight)
+      const uint8_t* rb = tbase;
+      auto ld = [&](int s, uint32_t (&w)[CW]) {
+        if (FULL) load_chunk<LAYOUT>(rb + voff, rb + hb + voff, plane, w);
+        else
+          load_chunk<LAYOUT>(s < vsteps ? pf + (int64_t)s * rowstep : pf,
+                             s < vstepsb ? pf + hb + (int64_t)s * rowstep : pf, plane, w);
+      };
       uint32_t wa[CW], wb[CW];
-      load_chunk<LAYOUT>(row_ptr(0), row_ptr_b(0), plane, wa);
+      ld(0, wa);
       for (int s = 0; s < steps; s += 2) {
         if (FULL && s + 1 < steps) rb += rowstep;
-        load_chunk<LAYOUT>(row_ptr(s + 1), row_ptr_b(s + 1), plane, wb);
+        ld(s + 1, wb);
         step(wa, s);
         if (s + 1 >= steps) break;
         if (FULL && s + 2 < steps) rb += rowstep;
-        load_chunk<LAYOUT>(row_ptr(s + 2), row_ptr_b(s + 2), plane, wa);
+        ld(s + 2, wa);
         step(wb, s + 1);
       }
     };
     if (full) run(std::true_type{});
     else run(std::false_type{});
     while (qn > 0) drain(qn < 64 ? qn : 64);
-    unpack_exc();
     Qa += Ba;
     Qb += Bb;
 
-    uint32_t acc[3 * NR];
+    uint32_t acc[12] = {};
 #pragma unroll
     for (int rr = 0; rr < NR; ++rr) {
       const int sh = 8 * rr;
@@ -869,29 +888,13 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         wx += __umul24(dx, nb2);
       }
       const uint32_t qq = ((rr & 1) ? (Qb >> ((rr >> 1) * 16)) : (Qa >> ((rr >> 1) * 16))) & 0xFFFFu;
-      acc[3 * rr + 0] = c + xacc[3 * rr + 0];
-      acc[3 * rr + 1] = __umul24(x0, c) + wx + xacc[3 * rr + 1];
+      acc[3 * rr + 0] = c;
+      acc[3 * rr + 1] = __umul24(x0, c) + wx;
       acc[3 * rr + 2] = __umul24((uint32_t)y0, c) + (uint32_t)g.rstep * ((uint32_t)steps * c - qq) +
-                        __umul24((uint32_t)half, nb2) + xacc[3 * rr + 2];
+                        __umul24((uint32_t)half, nb2);
     }
-    uint32_t red[12];
-#pragma unroll
-    for (int v = 0; v < 12; ++v) red[v] = v < 3 * NR ? acc[v] : 0u;
-    wave_sums12(red);
-    // lane 16 r + 15 holds values 3 r .. 3 r + 2: range r's N, sum x, sum y
-    const int rr = lane >> 4;
-    // the frame's sums: device atomics (fire and forget: no wave waits for
-    // another); fused step: the workgroup's totals in LDS
-    if ((lane & 15) == 15 && rr < NR) {
-      unsigned long long* dst =
-          reinterpret_cast<unsigned long long*>(&a.sums[(int64_t)f * a.sums_ranges + a.range_offset + rr].points);
-#pragma unroll
-      for (int v = 0; v < 3; ++v)
-        if (red[v]) {
-          atomicAdd(dst + v, (unsigned long long)red[v]);
-          if (a.fused) lds_add_u64(kLdsTotals + 8u * (uint32_t)(3 * rr + v), red[v]);
-        }
-    }
+    unpack_exc(acc);
+    emit(acc);
     u = __builtin_amdgcn_readfirstlane(next) + U;
   }
   // the exact-path word count: per workgroup in LDS, one device atomic by its
