@@ -75,6 +75,9 @@ def parse():
     ap.add_argument("--cpu-frames-emul", type=int, default=32,
                     help="sample of the oracle's intrinsic-level emulation (secondary rate)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--event-every", type=int, default=4,
+                    help="bracket every n-th timed step with HIP events for kernel_ms (an event record is a "
+                         "stream packet of a few us: on every step it would inflate ms_per_step)")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the cold-batch and scene measurements (PMC passes: only the bench's own launches)")
     ap.add_argument("--hot", choices=["auto", "stripe", "chroma"], default="auto",
@@ -298,19 +301,23 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    every = max(1, args.event_every)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+           for _ in range(0, args.steps, every)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(*evs[k])
+        if k % every == 0:
+            step(*evs[k // every])
+        else:
+            step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
     kind = det.last_hot_kernel()
     kname = {trik_hsv.HOT_CHROMA: "chroma_kernel", trik_hsv.HOT_STRIPE: "stripe_kernel",
              trik_hsv.HOT_GENERIC: "reduce_kernel", trik_hsv.HOT_MIXED: "mixed"}.get(kind, "?")
@@ -348,7 +355,8 @@ def main():
                      "traffic": traffic, "traffic_source": traffic_source,
                      "kernel": f"{kname}<YUYV,{T}>", "kernel_ms": round(kern_ms, 4),
                      "kernel_ms_max_rank": round(kern_ms_max, 4),
-                     "kernel_scope": ("the step's one launch (fused: sums stored, targets and totals written "
+                     "kernel_ms_launches": len(evs), "kernel_ms_event_every": every,
+                     "kernel_scope": ("the step's one launch (fused: its frames' sums zeroed and added, targets and totals written "
                                       "by the same kernel)" if fused else
                                       "the step's launches (zero the sums, hot kernel, epilogue, totals)"),
                      "bytes_per_launch": bytes_per_launch},

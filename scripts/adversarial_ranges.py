@@ -81,9 +81,11 @@ def time_case(frames, F, W, H, ranges, reps=20):
         det.batch_sums(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, ranges, sums, stream=stream)
         if hot == trik_hsv.HOT_CHROMA:
             expected = det.chroma_flagged_share()
-        for _ in range(5):
+        # warm-up, synchronised per call: AUTO reads the measured share back
+        # every few launches (trik_hsv_abi.cpp: probe_measured / poll_measured)
+        for _ in range(5 if hot != trik_hsv.HOT_AUTO else 40):
             det.batch_sums(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, ranges, sums, stream=stream)
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(reps):
@@ -92,6 +94,8 @@ def time_case(frames, F, W, H, ranges, reps=20):
         torch.cuda.synchronize()
         ran = {trik_hsv.HOT_CHROMA: "chroma", trik_hsv.HOT_STRIPE: "stripe",
                trik_hsv.HOT_MIXED: "mixed"}.get(det.last_hot_kernel(), "?")
+        if hot == trik_hsv.HOT_AUTO:
+            ran += f"[m={det.chroma_measured_share():.3f}]"
         out.append((["auto", "stripe", "chroma"][hot], ran, e0.elapsed_time(e1) / reps))
     det.close()
     return expected, out

@@ -57,7 +57,8 @@ static void sym(void* so, const char* name, F& f) {
 int main(int argc, char** argv) {
   int frames = 4096, W = 640, H = 480, T = 4, kind = 0, iters = 20, rounds = 3, hot = 2, layout = 0, full = 0;
   int opt;
-  while ((opt = getopt(argc, argv, "f:w:h:t:k:n:r:m:l:s")) != -1) {
+  int b2b = 0;
+  while ((opt = getopt(argc, argv, "f:w:h:t:k:n:r:m:l:sb")) != -1) {
     switch (opt) {
       case 'f': frames = atoi(optarg); break;
       case 'w': W = atoi(optarg); break;
@@ -69,6 +70,7 @@ int main(int argc, char** argv) {
       case 'm': hot = atoi(optarg); break;
       case 'l': layout = atoi(optarg); break;
       case 's': full = 1; break;  // time the full step (trik_hsv_process_batch_totals)
+      case 'b': b2b = 1; break;   // also back to back: per step without and with per-launch events
       default: return 2;
     }
   }
@@ -147,6 +149,39 @@ int main(int argc, char** argv) {
         L.ms.push_back(ms);
       }
     }
+  if (b2b) {  // steps enqueued back to back (as bench.py's timed loop), K = 200
+    const int K = 200;
+    std::vector<hipEvent_t> ev(2 * K);
+    for (auto& e : ev) CK(hipEventCreate(&e));
+    for (Lib& L : libs) {
+      auto launch = [&]() { (full ? L.step(L.h, &b, all, T, d_sums, d_targets, d_totals, s) : L.sums(L.h, &b, all, T, d_sums, s)); };
+      for (int w = 0; w < 10; ++w) launch();
+      CK(hipStreamSynchronize(s));
+      CK(hipEventRecord(e0, s));
+      for (int k = 0; k < K; ++k) launch();
+      CK(hipEventRecord(e1, s));
+      CK(hipEventSynchronize(e1));
+      float bare = 0;
+      CK(hipEventElapsedTime(&bare, e0, e1));
+      CK(hipEventRecord(e0, s));
+      for (int k = 0; k < K; ++k) {
+        CK(hipEventRecord(ev[2 * k], s));
+        launch();
+        CK(hipEventRecord(ev[2 * k + 1], s));
+      }
+      CK(hipEventRecord(e1, s));
+      CK(hipEventSynchronize(e1));
+      float with = 0, kern = 0;
+      CK(hipEventElapsedTime(&with, e0, e1));
+      for (int k = 0; k < K; ++k) {
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]));
+        kern += ms;
+      }
+      printf("%-40s back to back: %.4f ms/step bare, %.4f ms/step with per-launch events, launch %.4f ms, gap %.2f us\n",
+             L.path.c_str(), bare / K, with / K, kern / K, 1e3 * (with - kern) / K);
+    }
+  }
   const double bytes = (double)fb * frames;
   for (Lib& L : libs) {
     std::vector<float> v = L.ms;

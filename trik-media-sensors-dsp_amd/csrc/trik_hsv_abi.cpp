@@ -143,17 +143,69 @@ std::string validate_batch(const TrikHsvFrameBatch* b) {
 // streams: the last use on each stream is an event, so that a later call can
 // make its stream wait for them (device side) or, before the buffer is
 // rewritten, find out without blocking whether they have finished.
+// One event per stream the handle has enqueued work on, recorded once per
+// call after its last launch (an event record is a packet on the stream that
+// costs the GPU a few microseconds between kernels: one per call, not one per
+// buffer).  A new stream takes over the event of one whose recorded work has
+// completed once kMaxMarks streams are tracked, so the list stays bounded
+// however many short-lived streams a caller cycles through.
+constexpr size_t kMaxMarks = 16;
+struct StreamMarks {
+  std::vector<std::pair<hipStream_t, hipEvent_t>> marks;
+  int32_t mark(hipStream_t s, hipEvent_t* out) {
+    std::pair<hipStream_t, hipEvent_t>* slot = nullptr;
+    for (auto& m : marks)
+      if (m.first == s) {
+        slot = &m;
+        break;
+      }
+    if (!slot && marks.size() >= kMaxMarks)
+      for (auto& m : marks)
+        if (hipEventQuery(m.second) == hipSuccess) {
+          m.first = s;
+          slot = &m;
+          break;
+        }
+    if (!slot) {
+      hipEvent_t e = nullptr;
+      hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+      if (r != hipSuccess) return (int32_t)r;
+      marks.emplace_back(s, e);
+      slot = &marks.back();
+    }
+    *out = slot->second;
+    return (int32_t)hipEventRecord(slot->second, s);
+  }
+  void release() {
+    for (auto& m : marks) {
+      (void)hipEventSynchronize(m.second);
+      (void)hipEventDestroy(m.second);
+    }
+    marks.clear();
+  }
+};
+
+// The streams whose enqueued work reads or writes a buffer, each with the
+// handle's event for that stream (StreamMarks, not owned here) recorded after
+// that work.  The event may since have been recorded again, after later work:
+// the tests below are conservative, never early.
 struct StreamUses {
   std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
-  // the calling stream has (just) enqueued work that reads or writes the buffer
-  int32_t note(hipStream_t s) {
-    for (auto& u : uses)
-      if (u.first == s) return (int32_t)hipEventRecord(u.second, s);
-    hipEvent_t e = nullptr;
-    hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
-    if (r != hipSuccess) return (int32_t)r;
-    uses.emplace_back(s, e);
-    return (int32_t)hipEventRecord(e, s);
+  // the calling stream has (just) enqueued work on the buffer; e: its mark
+  void note(hipStream_t s, hipEvent_t e) {
+    bool found = false;
+    size_t j = 0;
+    for (size_t i = 0; i < uses.size(); ++i) {
+      if (uses[i].first == s) {
+        uses[i].second = e;
+        found = true;
+      } else if (uses[i].second == e) {
+        continue;  // the event moved to stream s: that stream's work completed
+      }
+      uses[j++] = uses[i];
+    }
+    uses.resize(j);
+    if (!found) uses.emplace_back(s, e);
   }
   // every recorded use has completed (non-blocking)
   bool idle() const {
@@ -173,10 +225,7 @@ struct StreamUses {
   void wait_all() const {
     for (const auto& u : uses) (void)hipEventSynchronize(u.second);
   }
-  void release() {
-    for (auto& u : uses) (void)hipEventDestroy(u.second);
-    uses.clear();
-  }
+  void release() { uses.clear(); }
 };
 
 // Compiled range tables (device) for one range set, with the key (packed
@@ -319,6 +368,7 @@ struct TrikCvHandle {
   TrikHsvTarget* d_blob_targets = nullptr;
   size_t d_blob_targets_cap = 0;
   StreamUses blob_users;  // calls that wrote the multi-blob scratch
+  StreamMarks marks;      // the events the StreamUses lists point at (freed last)
 };
 
 namespace {
@@ -337,6 +387,7 @@ void free_resources(TrikCvHandle* h) {
   h->blob_users.release();
   h->fused_users.wait_all();
   h->fused_users.release();
+  h->marks.release();
   (void)hipFree(h->d_wg_part);
   (void)hipFree(h->d_frame);
   (void)hipFree(h->d_maps);
@@ -602,6 +653,18 @@ struct StepOut {
   TrikHsvTargetSums* totals = nullptr;
 };
 
+// Record that the work just enqueued on s reads `set` (and the preview maps,
+// and `extra`): one event record on s for the call.
+int32_t note_uses(TrikCvHandle* h, TableSet* set, bool maps, hipStream_t s, StreamUses* extra = nullptr) {
+  hipEvent_t e = nullptr;
+  int32_t r = h->marks.mark(s, &e);
+  if (r) return fail(TRIK_IVIDTRANSCODE_EFAIL, std::string("hipEventRecord: ") + hipGetErrorString((hipError_t)r));
+  if (set) set->users.note(s, e);
+  if (maps) h->maps_users.note(s, e);
+  if (extra) extra->note(s, e);
+  return 0;
+}
+
 // The fused step's scratch (one slot of 12 totals per CU, the counter zeroed
 // once), allocated on first use.
 int32_t ensure_fused_scratch(TrikCvHandle* h, hipStream_t s) {
@@ -738,9 +801,7 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
     if (step->targets) HIP_TRY(launch_targets(*b, n, sums, step->targets, s));
     if (step->totals) HIP_TRY(launch_totals(b->n_frames > 0 ? b->n_frames : 0, n, sums, step->totals, s));
   }
-  rc = t->users.note(s);
-  if (!rc && fused) rc = h->fused_users.note(s);
-  return rc ? fail(TRIK_IVIDTRANSCODE_EFAIL, std::string("hipEventRecord: ") + hipGetErrorString((hipError_t)rc)) : 0;
+  return note_uses(h, t, false, s, fused ? &h->fused_users : nullptr);
 }
 
 inline void set_bit(int32_t& word, int bit) { word |= (int32_t)(1u << bit); }
@@ -812,12 +873,6 @@ int32_t preview_tables(TrikCvHandle* h, PreviewArgs& pa, const TRIK_VIDTRANSCODE
   return 0;
 }
 
-// Record that the work just enqueued on s reads `set` (and the preview maps).
-int32_t note_uses(TrikCvHandle* h, TableSet* set, bool maps, hipStream_t s) {
-  int32_t r = set ? set->users.note(s) : 0;
-  if (!r && maps) r = h->maps_users.note(s);
-  return r ? fail(TRIK_IVIDTRANSCODE_EFAIL, std::string("hipEventRecord: ") + hipGetErrorString((hipError_t)r)) : 0;
-}
 
 // The line sensor's range in the object sensor's terms: hue 0..359 and
 // saturation 0..100 scale to the full 0..255 bytes LSEQ:391-396 fixes.
@@ -1304,8 +1359,7 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
           if (r) return r;
           r = run_blob(h, ba, *set, h->stream);
           if (r) return r;
-          r = note_uses(h, set, false, h->stream);
-          if (!r) r = h->blob_users.note(h->stream);
+          r = note_uses(h, set, false, h->stream, &h->blob_users);
           if (r) return r;
           if (out_ptr && out_size > 0) {  // preview: set metapixels, guide lines, target marks
             const size_t pb = (size_t)out_size;
@@ -1783,9 +1837,7 @@ extern "C" int32_t trik_hsv_blob_batch(TRIK_VIDTRANSCODE_CV_Handle h, const Trik
   if (r) return r;
   r = run_blob(h, ba, *set, s);
   if (r) return r;
-  r = note_uses(h, set, false, s);
-  if (!r) r = h->blob_users.note(s);
-  return r ? fail(TRIK_IVIDTRANSCODE_EFAIL, "hipEventRecord failed") : 0;
+  return note_uses(h, set, false, s, &h->blob_users);
 }
 
 extern "C" int32_t trik_hsv_blob_preview(TRIK_VIDTRANSCODE_CV_Handle h, const TrikHsvFrameBatch* b,

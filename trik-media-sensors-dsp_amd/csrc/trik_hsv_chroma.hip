@@ -604,10 +604,11 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
                                                  1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     // (the divisions run on the VALU: their wave-uniform results are moved to
     // SGPRs, else everything derived from them stays in VGPRs)
+    // (tile indices fit 32 bits: chroma_geometry)
     const uint32_t tl = __builtin_amdgcn_readfirstlane(u / U);
-    const int64_t tile = t_begin + tl;
-    const int f = __builtin_amdgcn_readfirstlane((int)(tile / g.tiles_per_frame));
-    const int trem = __builtin_amdgcn_readfirstlane((int)(tile - (int64_t)f * g.tiles_per_frame));
+    const uint32_t tile = (uint32_t)t_begin + tl;
+    const int f = (int)__builtin_amdgcn_readfirstlane(tile / (uint32_t)g.tiles_per_frame);
+    const int trem = (int)(tile - (uint32_t)f * (uint32_t)g.tiles_per_frame);
     const int lt = (int)((u - tl * U) * 64u) + lane;  // the lane's index in the tile
     const bool active = lt < g.k * g.cpr;
     const int col = active ? lt % g.cpr : 0;
@@ -1157,6 +1158,7 @@ bool chroma_geometry(const KernelArgs& a, ChromaGeom& g) {
   g.tiles_per_frame = (steps_total + g.steps - 1) / g.steps;  // every tile has >= 1 step
   g.steps_last = steps_total - (g.tiles_per_frame - 1) * g.steps;
   g.n_tiles = (int64_t)g.tiles_per_frame * a.n_frames;
+  if (g.n_tiles * ((g.k * g.cpr + 63) / 64) > 0xFFFFFFFFll) return false;  // 32-bit tile and unit indices
   // per drain round a lane adds <= 2 pixels: byte counts <= 2r, x sums <= 2r*W,
   // row sums <= 2r*rows; the 16-bit sums must take at least one round
   const int rows = g.steps * g.rstep;
