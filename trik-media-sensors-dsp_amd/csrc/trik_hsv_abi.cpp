@@ -538,14 +538,35 @@ int32_t acquire_tables(TrikCvHandle* h, const TRIK_VIDTRANSCODE_CV_InArgsAlg* ra
   // the set's earlier uploads and readers have finished (idle), so its pinned
   // staging and device tables may be rewritten
   v->detect.assign(groups, kDetectFull);
+  // the tables: built on the device from the packed ranges (no table crosses
+  // PCIe: a host-built upload went through the copy engine, whose hand-offs
+  // with the compute queue cost tens of microseconds); the per-value tests
+  // are also compiled on the host, for detect_mode
+  TableBuildArgs ta = {};
+  ta.n_ranges = n;
+  for (int i = 0; i < n && groups <= kTableGroups; ++i) {
+    const PackedRange p = pack_range(ranges[i]);
+    ta.from[i] = p.from;
+    ta.to[i] = p.to;
+    ta.expect[i] = p.expect;
+  }
   for (int g = 0; g < groups; ++g) {
     const int cnt = n - g * kRangesPerLaunch < kRangesPerLaunch ? n - g * kRangesPerLaunch : kRangesPerLaunch;
-    compile_tables(ranges + g * kRangesPerLaunch, cnt, &v->h_tables[g]);
-    compile_stripe_tables(v->h_tables[g], cnt, &v->h_stripe[g]);
+    if (groups <= kTableGroups) {
+      compile_tables_head(ranges + g * kRangesPerLaunch, cnt, &v->h_tables[g]);
+    } else {  // (more than 64 ranges: compiled on the host, uploaded below)
+      compile_tables(ranges + g * kRangesPerLaunch, cnt, &v->h_tables[g]);
+      compile_stripe_tables(v->h_tables[g], cnt, &v->h_stripe[g]);
+    }
     v->detect[g] = (uint8_t)detect_mode(v->h_tables[g], cnt);
   }
-  HIP_TRY(hipMemcpyAsync(v->d_tables, v->h_tables, sizeof(RangeTables) * groups, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(v->d_stripe, v->h_stripe, sizeof(StripeTables) * groups, hipMemcpyHostToDevice, s));
+  if (groups == 0) {
+  } else if (groups <= kTableGroups) {
+    HIP_TRY(launch_compile_tables(ta, groups, v->d_tables, v->d_stripe, s));
+  } else {
+    HIP_TRY(hipMemcpyAsync(v->d_tables, v->h_tables, sizeof(RangeTables) * groups, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(v->d_stripe, v->h_stripe, sizeof(StripeTables) * groups, hipMemcpyHostToDevice, s));
+  }
   HIP_TRY(hipEventRecord(v->ready, s));
   v->key.swap(key);
   v->chroma_built = false;

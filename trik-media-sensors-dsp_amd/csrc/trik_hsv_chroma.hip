@@ -203,45 +203,97 @@ __device__ __forceinline__ uint32_t spread4(uint32_t m) { return (m * 0x00204081
 // chroma index U | V << 8 of a YUYV word (b0=Y0, b1=U, b2=Y1, b3=V)
 __device__ __forceinline__ uint32_t chroma_of(uint32_t w) { return __builtin_amdgcn_perm(w, w, 0x0C0C0301u); }
 
+// The exact mask (bit t = range t) of pixel PIX of YUYV word w: the stripe
+// kernel's arithmetic (trik_hsv_stripe_px.h: WSEQ:181-249 via v_dot4, the
+// 16-bit wrap in v_bfe) with LUT43/LUT255 and the H, S, V tests from LDS.
+template <int PIX>
+__device__ __forceinline__ uint32_t exact_mask(uint32_t w) {
+  constexpr uint32_t kY = PIX == 0 ? 74u : (74u << 16);
+  const uint32_t wc = w ^ 0xFF00FF00u;
+  const int r = stripe_px::clamp8_shift6(__builtin_amdgcn_udot4(w, kY | (102u << 24), (uint32_t)-14248, false));
+  const int g = stripe_px::clamp8_shift6(
+      __builtin_amdgcn_udot4(wc, kY | (25u << 8) | (52u << 24), (uint32_t)-10939, false));
+  const int b = stripe_px::clamp8_shift6(__builtin_amdgcn_udot4(w, kY | (129u << 8), (uint32_t)-17672, false));
+  const int mx = max(r, max(g, b)), mn = min(r, min(g, b));
+  const uint32_t d = (uint32_t)(mx - mn);
+  const int m = (int)ld16(kLdsLut43 + 2u * d);
+  const uint32_t S = (ld16(kLdsLut255 + 2u * (uint32_t)mx) * d) >> 8;
+  // hue case select as in stripe_px::phase1 (G > B > R on ties), branch-free
+  const bool eqG = mx == g, eqB = mx == b;
+  const int dR = g - b, dG = b - r, dB = r - g;
+  const int diff = eqG ? dG : (eqB ? dB : dR);
+  const int base = eqG ? 21845 : (eqB ? 43690 : 0);
+  const uint32_t H = ((uint32_t)(base + m * diff) >> 8) & 0xFFu;
+  return ld8(kLdsHue + H) & ld8(kLdsSat + S) & ld8(kLdsVal + (uint32_t)mx);
+}
+
 // ---------------------------------------------------------------------------
 // Builder
 // ---------------------------------------------------------------------------
-// One thread per chroma (block = V, thread = U): the exact T-bit mask for
-// every Y (the trik_hsv_pixel.h arithmetic, held to the oracle on all 2^24
-// triples by the exhaustive tests) -- the chroma's profile -- summarised as
-// its runs with the trailing zero run removed:
+// The exact-path tables (LUT43, LUT255, per-value H, S, V range masks) at
+// their LDS image addresses (exact_mask reads them there).
+__device__ __forceinline__ void stage_exact_tables(const RangeTables* t, int tid, int n) {
+  for (int i = tid; i < 256; i += n) {
+    *(lds16_t)(uintptr_t)(kLdsLut43 + 2 * i) = t->lut43[i];
+    *(lds16_t)(uintptr_t)(kLdsLut255 + 2 * i) = t->lut255[i];
+    *(lds8_t)(uintptr_t)(kLdsHue + i) = t->hue[i];
+    *(lds8_t)(uintptr_t)(kLdsSat + i) = t->smask[i];
+    *(lds8_t)(uintptr_t)(kLdsVal + i) = t->vmask[i];
+  }
+}
+
+// One workgroup of 1024 per V: the exact T-bit mask of every (Y, U) -- the
+// 256 chromas' profiles, two Y per YUYV word through exact_mask (the stripe
+// kernel's arithmetic on LDS tables, held to the oracle on all 2^24 triples)
+// into LDS -- then one thread per chroma summarises its profile's runs with
+// the trailing zero run removed:
 //   bits 0-1 number of runs (3 = more than two), 4-7 v1, 8-11 v2,
 //   12-20 end of run 1, 21-29 end of run 2 (two runs) or of the last nonzero
 //   run (more than two).
-// One workgroup per (V, quarter of the U range): 256 threads evaluate the
-// 64 chromas' masks for a quarter of the Y range each into LDS, then one
-// thread per chroma walks its 256 masks.
-__global__ __launch_bounds__(256) void chroma_summary_kernel(const RangeTables* t, ChromaTables* ct) {
-  __shared__ uint8_t prof[64][256 + 4];  // [chroma][Y], rows padded against bank conflicts
-  const int V = blockIdx.x >> 2, U0 = (blockIdx.x & 3) * 64;
-  {
-    const int u = threadIdx.x & 63, y0 = (threadIdx.x >> 6) * 64;
-    for (int y = y0; y < y0 + 64; ++y) prof[u][y] = (uint8_t)detect_pixel(y, U0 + u, V, *t);
+constexpr uint32_t kSumStride = 260;  // profile rows, padded against bank conflicts
+constexpr uint32_t kSumProf = 16384;  // [256][kSumStride] u8, after the exact tables
+constexpr uint32_t kSumLds = kSumProf + 256 * kSumStride;
+static_assert(kLdsVal + 256 <= kSumProf && kSumLds <= 160 * 1024, "summary LDS image");
+__global__ __launch_bounds__(1024) void chroma_summary_kernel(const RangeTables* t, ChromaTables* ct) {
+  const uint32_t V = blockIdx.x, tid = threadIdx.x;
+  stage_exact_tables(t, (int)tid, (int)blockDim.x);
+  if (V == 0 && tid == 0) {  // summed by the block kernel's palette pass; the hot kernel's count
+    ct->flagged_cost = 0ull;
+    ct->flagged_words = 0ull;
   }
   __syncthreads();
-  if (threadIdx.x >= 64) return;
-  const int U = U0 + (int)threadIdx.x;
-  const uint8_t* row = prof[threadIdx.x];
-  const uint32_t c = (uint32_t)U | ((uint32_t)V << 8);
+  {  // lane U of a wave, 32 Y pairs per thread
+    const uint32_t U = tid & 255u, j0 = (tid >> 8) * 32u;
+    const uint32_t row = kSumProf + U * kSumStride;
+    for (uint32_t j = j0; j < j0 + 32u; ++j) {
+      const uint32_t w = (2u * j) | (U << 8) | ((2u * j + 1u) << 16) | (V << 24);
+      *(lds16_t)(uintptr_t)(row + 2u * j) = (uint16_t)(exact_mask<0>(w) | (exact_mask<1>(w) << 8));
+    }
+  }
+  __syncthreads();
+  if (tid >= 256u) return;
+  const uint32_t U = tid;
+  const uint32_t row = kSumProf + U * kSumStride;
+  const uint32_t c = U | (V << 8);
   int nruns = 0;            // runs so far, including the current one
   uint32_t vals[3] = {0, 0, 0};
   int ends[3] = {0, 0, 0};  // exclusive end of each run
   uint32_t cur = 0xFFu;
   int last_nz_run = -1, last_nz_end = 0;
-  for (int Y = 0; Y < 256; ++Y) {
-    const uint32_t m = row[Y];
-    if (m != cur) {
-      if (nruns < 3) vals[nruns] = m;
-      ++nruns;
-      cur = m;
+  for (int Y4 = 0; Y4 < 256; Y4 += 4) {
+    const uint32_t q = *(lds32_t)(uintptr_t)(row + (uint32_t)Y4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int Y = Y4 + k;
+      const uint32_t m = (q >> (8 * k)) & 0xFFu;
+      if (m != cur) {
+        if (nruns < 3) vals[nruns] = m;
+        ++nruns;
+        cur = m;
+      }
+      if (nruns <= 3) ends[nruns - 1] = Y + 1;
+      if (m) { last_nz_run = nruns - 1; last_nz_end = Y + 1; }
     }
-    if (nruns <= 3) ends[nruns - 1] = Y + 1;
-    if (m) { last_nz_run = nruns - 1; last_nz_end = Y + 1; }
   }
   // runs up to and including the last nonzero one
   const int n = last_nz_run + 1;  // 0: all zero
@@ -253,11 +305,12 @@ __global__ __launch_bounds__(256) void chroma_summary_kernel(const RangeTables* 
     return (uint32_t)(nn > 2 ? 3 : nn) | (v1 << 4) | ((nn == 2 ? v2 : 0u) << 8) | ((uint32_t)a << 12) |
            ((uint32_t)ab << 21);
   };
-  ct->summary[c] = pack(n, vals[0], vals[1], ends[0]);
+  const uint32_t sf = pack(n, vals[0], vals[1], ends[0]);
+  ct->summary[c] = sf;
   // the profile from its first nonzero Y on: without a leading zero run the
   // same; with one, the runs after it (runs 1 and 2 become runs 0 and 1)
   const bool lead0 = vals[0] == 0u && n > 0;
-  ct->summary_drop[c] = lead0 ? pack(n - 1, vals[1], vals[2], ends[1]) : ct->summary[c];
+  ct->summary_drop[c] = lead0 ? pack(n - 1, vals[1], vals[2], ends[1]) : sf;
   ct->first_nz[c] = (uint16_t)(n == 0 ? 256 : (lead0 ? ends[0] : 0));
 }
 
@@ -308,137 +361,136 @@ __device__ __forceinline__ uint32_t chroma_desc_cut(uint32_t sf, uint32_t sd, ui
   return chroma_desc(f == A ? sd : sf, k & 15u, k >> 4);
 }
 
-// One workgroup per 16-chroma block b = (V << 4) | (U >> 4): the candidate
-// mask pairs k = M1 | M2 << 4 and cuts A (0, or the first nonzero Y of one of
-// the block's chromas) are listed in LDS and their combinations spread over
-// the 256 threads; the workgroup keeps the (cost, k, A) with the fewest
-// expected exact-path words over the block (ties: smaller k, then smaller A).
-// PALETTE = false: all pairs whose masks occur in the block; the choice is
-// counted in pair_hist.  PALETTE = true: the palette's pairs only (the same
-// choice when the unrestricted pair made the palette, which is nearly
-// always); then the block word (the pair's palette offset | the cut << 8)
-// and the run descriptors.
+// One wave per 16-chroma block b = (V << 4) | (U >> 4), 16 blocks per
+// workgroup: the candidate mask pairs k = M1 | M2 << 4 and cuts A (0, or the
+// first nonzero Y of one of the block's chromas) are listed in the wave's LDS
+// and their combinations spread over its 64 lanes; the wave keeps the
+// (cost, k, A) with the fewest expected exact-path words over the block
+// (ties: smaller k, then smaller A).
+// PALETTE = false: all pairs whose masks occur in the block (best[b]).
+// PALETTE = true: every workgroup first ranks the pairs the first pass chose
+// (from best[], in LDS; workgroup 0 stores the result): the palette is the
+// (up to) kChromaPalette most used pairs (ties: the smaller k), palette_of[k]
+// = 8 * slot or 0xFF, with the byte-spread pair of each slot.  Then the
+// palette's pairs only (the same choice when the unrestricted pair made the
+// palette, which is nearly always), the block word (the pair's palette offset
+// | the cut << 8), the run descriptors, and the blocks' expected exact-path
+// words added into flagged_cost (one atomic per workgroup).
+constexpr int kBlocksPerGroup = 16;
 template <bool PALETTE>
-__global__ __launch_bounds__(256) void chroma_block_kernel(ChromaTables* ct) {
-  __shared__ uint32_t sf[16], sd[16], fz[16];
-  __shared__ uint32_t pairs[256], cuts[17];
-  __shared__ uint32_t n_pairs, n_cuts;
-  __shared__ unsigned long long best;
-  const int b = blockIdx.x;
-  const uint32_t t = threadIdx.x;
+__global__ __launch_bounds__(1024) void chroma_block_kernel(ChromaTables* ct) {
+  __shared__ uint32_t sf[kBlocksPerGroup][16], sd[kBlocksPerGroup][16], fz[kBlocksPerGroup][16];
+  __shared__ uint32_t pairs[kBlocksPerGroup][256], cuts[kBlocksPerGroup][17];
+  __shared__ uint32_t hist[256];
+  __shared__ uint8_t pal_of[256];
+  __shared__ unsigned long long part[kBlocksPerGroup];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  const int b = (int)(blockIdx.x * kBlocksPerGroup + wv);
   const uint32_t c0 = ((uint32_t)(b >> 4) << 8) | ((uint32_t)(b & 15) << 4);
-  if (t < 16) {
-    sf[t] = ct->summary[c0 + t];
-    sd[t] = ct->summary_drop[c0 + t];
-    fz[t] = ct->first_nz[c0 + t];
+  if (lane < 16) {
+    sf[wv][lane] = ct->summary[c0 + lane];
+    sd[wv][lane] = ct->summary_drop[c0 + lane];
+    fz[wv][lane] = ct->first_nz[c0 + lane];
   }
-  if (t == 0) {
-    best = ~0ull;
-    n_pairs = 0;
-    // the palette pass: when this block's unrestricted choice (pass 1) made
-    // the palette, it is also the cheapest palette choice (the same keys over
-    // a subset that contains it) -- no second search
-    if (PALETTE) {
-      const unsigned long long b1 = ct->best[b];
-      if (ct->palette_of[(uint32_t)(b1 >> 9) & 255u] != 0xFFu) best = b1;
-    }
-  }
-  __syncthreads();
-  const bool known = PALETTE && best != ~0ull;  // uniform across the block
-  if (!known) {
-    if (t == 0) {  // the cuts: 0, then each chroma's first nonzero Y in (0, 255]
-      uint32_t n = 0;
-      cuts[n++] = 0;
-      for (int j = 0; j < 16; ++j)
-        if (fz[j] != 0u && fz[j] <= 255u) cuts[n++] = fz[j];
-      n_cuts = n;
-    }
-    {  // the pairs: thread t stands for pair k = t
-      const uint32_t k = t;
-      bool take;
-      if (PALETTE) {
-        take = ct->palette_of[k] != 0xFFu;
-      } else {
-        uint32_t present = 1u;  // mask values appearing (value 0 always a candidate)
-        for (int i = 0; i < 16; ++i) {
-          if (sf[i] & 3u) present |= 1u << ((sf[i] >> 4) & 15u);
-          if ((sf[i] & 3u) == 2u) present |= 1u << ((sf[i] >> 8) & 15u);
-          if (sd[i] & 3u) present |= 1u << ((sd[i] >> 4) & 15u);
-          if ((sd[i] & 3u) == 2u) present |= 1u << ((sd[i] >> 8) & 15u);
-        }
-        take = ((present >> (k & 15u)) & 1u) && ((present >> (k >> 4)) & 1u);
+  if (PALETTE) {  // the palette, from the first pass's choices
+    if (tid < 256u) hist[tid] = 0u;
+    __syncthreads();
+    for (uint32_t i = tid; i < 4096u; i += blockDim.x) atomicAdd(&hist[(uint32_t)(ct->best[i] >> 9) & 255u], 1u);
+    __syncthreads();
+    if (tid < 256u) {
+      const uint32_t k = tid, n = hist[k];
+      uint32_t rank = 0;
+      for (uint32_t j = 0; j < 256; ++j) {
+        const uint32_t m = hist[j];
+        rank += (m > n) | ((m == n) & (j < k));
       }
-      if (take) pairs[atomicAdd(&n_pairs, 1u)] = k;  // order does not matter: the key decides
+      const bool in = n > 0 && rank < (uint32_t)kChromaPalette;
+      pal_of[k] = in ? (uint8_t)(8u * rank) : (uint8_t)0xFFu;
+      if (blockIdx.x == 0) {
+        ct->pair_hist[k] = n;
+        ct->palette_of[k] = pal_of[k];
+        if (in) {
+          ct->palette[2 * rank] = spread4(k & 15u);
+          ct->palette[2 * rank + 1] = spread4(k >> 4);
+        }
+      }
     }
     __syncthreads();
-    const uint32_t np = n_pairs, nc = n_cuts;
+  } else {
+    __builtin_amdgcn_wave_barrier();
+  }
+  unsigned long long best = ~0ull;
+  // the palette pass: when this block's unrestricted choice (pass 1) made the
+  // palette, it is also the cheapest palette choice (the same keys over a
+  // subset that contains it) -- no second search
+  if (PALETTE) {
+    const unsigned long long b1 = ct->best[b];
+    if (pal_of[(uint32_t)(b1 >> 9) & 255u] != 0xFFu) best = b1;
+  }
+  if (best == ~0ull) {  // (wave-uniform)
+    // the cuts: 0, then each chroma's first nonzero Y in (0, 255]
+    const uint32_t f = lane < 16 ? fz[wv][lane] : 0u;
+    const uint64_t cm = __builtin_amdgcn_ballot_w64(lane < 16 && f != 0u && f <= 255u);
+    if (lane == 0) cuts[wv][0] = 0u;
+    if ((cm >> lane) & 1u) cuts[wv][1 + __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u)] = f;
+    const uint32_t nc = 1u + (uint32_t)__builtin_popcountll(cm);
+    // the pairs: lane l stands for pairs l, l + 64, l + 128, l + 192
+    uint32_t present = 1u;  // mask values appearing (value 0 always a candidate)
+    if (!PALETTE) {
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t a = sf[wv][i], d = sd[wv][i];
+        if (a & 3u) present |= 1u << ((a >> 4) & 15u);
+        if ((a & 3u) == 2u) present |= 1u << ((a >> 8) & 15u);
+        if (d & 3u) present |= 1u << ((d >> 4) & 15u);
+        if ((d & 3u) == 2u) present |= 1u << ((d >> 8) & 15u);
+      }
+    }
+    uint32_t np = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t k = lane + 64u * (uint32_t)q;
+      const bool take = PALETTE ? pal_of[k] != 0xFFu
+                                : (((present >> (k & 15u)) & 1u) && ((present >> (k >> 4)) & 1u));
+      const uint64_t pm = __builtin_amdgcn_ballot_w64(take);
+      if (take)
+        pairs[wv][np + __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u))] = k;
+      np += (uint32_t)__builtin_popcountll(pm);
+    }
+    __builtin_amdgcn_wave_barrier();
     unsigned long long mine = ~0ull;
-    for (uint32_t combo = t; combo < np * nc; combo += blockDim.x) {
-      const uint32_t k = pairs[combo / nc], A = cuts[combo % nc];
+    for (uint32_t combo = lane; combo < np * nc; combo += 64u) {
+      const uint32_t k = pairs[wv][combo / nc], A = cuts[wv][combo % nc];
       uint32_t cost = 0;
-      for (int i = 0; i < 16; ++i) cost += chroma_cost(chroma_desc_cut(sf[i], sd[i], fz[i], k, A));
+      for (int i = 0; i < 16; ++i) cost += chroma_cost(chroma_desc_cut(sf[wv][i], sd[wv][i], fz[wv][i], k, A));
       const unsigned long long key = ((unsigned long long)cost << 17) | ((unsigned long long)k << 9) | A;
       if (key < mine) mine = key;
     }
-    if (mine != ~0ull) atomicMin(&best, mine);
-    __syncthreads();
-  }
-  const uint32_t bk = (uint32_t)(best >> 9) & 255u, bA = (uint32_t)best & 511u;
-  if (!PALETTE) {
-    if (t == 0) {
-      ct->best[b] = best;  // chroma_palette_kernel histograms the pairs
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const unsigned long long o = __shfl_xor(mine, off, 64);
+      if (o < mine) mine = o;
     }
+    best = mine;
+  }
+  if (!PALETTE) {
+    if (lane == 0) ct->best[b] = best;  // the palette pass histograms the pairs
     return;
   }
-  if (t < 16) ct->runs[c0 + t] = (uint16_t)chroma_desc_cut(sf[t], sd[t], fz[t], bk, bA);
-  if (t == 0) {
-    ct->blocks[b] = (uint16_t)(ct->palette_of[bk] | (bA << 8));
-    ct->block_cost[b] = (uint32_t)(best >> 17);  // summed by chroma_cost_kernel (no same-address atomics)
+  const uint32_t bk = (uint32_t)(best >> 9) & 255u, bA = (uint32_t)best & 511u;
+  if (lane < 16) ct->runs[c0 + lane] = (uint16_t)chroma_desc_cut(sf[wv][lane], sd[wv][lane], fz[wv][lane], bk, bA);
+  if (lane == 0) {
+    ct->blocks[b] = (uint16_t)(pal_of[bk] | (bA << 8));
+    ct->block_cost[b] = (uint32_t)(best >> 17);
+    part[wv] = best >> 17;
   }
-}
-
-// One workgroup of 256: the palette is the (up to) kChromaPalette most used
-// pairs (ties: the smaller k); palette_of[k] = 8 * slot or 0xFF, and the
-// byte-spread pair of each slot.
-__global__ __launch_bounds__(256) void chroma_palette_kernel(ChromaTables* ct) {
-  __shared__ uint32_t hist[256];
-  const uint32_t k = threadIdx.x;
-  hist[k] = 0;
   __syncthreads();
-  for (uint32_t b = k; b < 4096; b += 256) atomicAdd(&hist[(uint32_t)(ct->best[b] >> 9) & 255u], 1u);
-  __syncthreads();
-  const uint32_t n = hist[k];
-  ct->pair_hist[k] = n;
-  uint32_t rank = 0;
-  for (uint32_t j = 0; j < 256; ++j) {
-    const uint32_t m = hist[j];
-    rank += (m > n) | ((m == n) & (j < k));
-  }
-  const bool in = n > 0 && rank < (uint32_t)kChromaPalette;
-  ct->palette_of[k] = in ? (uint8_t)(8u * rank) : (uint8_t)0xFFu;
-  if (in) {
-    ct->palette[2 * rank] = spread4(k & 15u);
-    ct->palette[2 * rank + 1] = spread4(k >> 4);
-  }
-}
-
-// One workgroup of 1024: flagged_cost = the sum of the blocks' costs.
-__global__ __launch_bounds__(1024) void chroma_cost_kernel(ChromaTables* ct) {
-  __shared__ unsigned long long part[16];
-  const uint32_t t = threadIdx.x;
-  unsigned long long v = 0;
-  for (uint32_t b = t; b < 4096; b += 1024) v += ct->block_cost[b];
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  if ((t & 63) == 0) part[t >> 6] = v;
-  __syncthreads();
-  if (t == 0) {
+  if (tid == 0) {
     unsigned long long sum = 0;
-    for (int i = 0; i < 16; ++i) sum += part[i];
-    ct->flagged_cost = sum;
-    ct->flagged_words = 0;
+    for (int i = 0; i < kBlocksPerGroup; ++i) sum += part[i];
+    atomicAdd(&ct->flagged_cost, sum);
   }
 }
+
 
 // ---------------------------------------------------------------------------
 // Hot kernel
@@ -505,30 +557,6 @@ __device__ __forceinline__ void load_chunk(const uint8_t* p, const uint8_t* pb, 
 }
 
 __device__ __forceinline__ uint32_t pack_bits(uint32_t e) { return ((e * 0x01020408u) >> 24) & 0xFu; }
-
-// The exact mask (bit t = range t) of pixel PIX of YUYV word w: the stripe
-// kernel's arithmetic (trik_hsv_stripe_px.h: WSEQ:181-249 via v_dot4, the
-// 16-bit wrap in v_bfe) with LUT43/LUT255 and the H, S, V tests from LDS.
-template <int PIX>
-__device__ __forceinline__ uint32_t exact_mask(uint32_t w) {
-  constexpr uint32_t kY = PIX == 0 ? 74u : (74u << 16);
-  const uint32_t wc = w ^ 0xFF00FF00u;
-  const int r = stripe_px::clamp8_shift6(__builtin_amdgcn_udot4(w, kY | (102u << 24), (uint32_t)-14248, false));
-  const int g = stripe_px::clamp8_shift6(
-      __builtin_amdgcn_udot4(wc, kY | (25u << 8) | (52u << 24), (uint32_t)-10939, false));
-  const int b = stripe_px::clamp8_shift6(__builtin_amdgcn_udot4(w, kY | (129u << 8), (uint32_t)-17672, false));
-  const int mx = max(r, max(g, b)), mn = min(r, min(g, b));
-  const uint32_t d = (uint32_t)(mx - mn);
-  const int m = (int)ld16(kLdsLut43 + 2u * d);
-  const uint32_t S = (ld16(kLdsLut255 + 2u * (uint32_t)mx) * d) >> 8;
-  // hue case select as in stripe_px::phase1 (G > B > R on ties), branch-free
-  const bool eqG = mx == g, eqB = mx == b;
-  const int dR = g - b, dG = b - r, dB = r - g;
-  const int diff = eqG ? dG : (eqB ? dB : dR);
-  const int base = eqG ? 21845 : (eqB ? 43690 : 0);
-  const uint32_t H = ((uint32_t)(base + m * diff) >> 8) & 0xFFu;
-  return ld8(kLdsHue + H) & ld8(kLdsSat + S) & ld8(kLdsVal + (uint32_t)mx);
-}
 
 // Per-lane sums of the exception pixels a lane drained: EN byte-packed counts
 // (range t in byte t), SX/SY 16-bit fields (ranges 0,2 | 1,3) of x and of the
@@ -1119,13 +1147,13 @@ int launch_nr(const KernelArgs& a, const ChromaGeom& g, const ChromaTables* ct, 
 }  // namespace
 
 int build_chroma_tables(const RangeTables* t, ChromaTables* ct, hipStream_t s) {
-  hipLaunchKernelGGL(chroma_summary_kernel, dim3(1024), dim3(256), 0, s, t, ct);
-  hipError_t e = hipGetLastError();
+  hipError_t e = set_dynamic_lds(reinterpret_cast<const void*>(chroma_summary_kernel), (int)kSumLds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(chroma_block_kernel<false>, dim3(4096), dim3(256), 0, s, ct);
-  hipLaunchKernelGGL(chroma_palette_kernel, dim3(1), dim3(256), 0, s, ct);
-  hipLaunchKernelGGL(chroma_block_kernel<true>, dim3(4096), dim3(256), 0, s, ct);
-  hipLaunchKernelGGL(chroma_cost_kernel, dim3(1), dim3(1024), 0, s, ct);
+  hipLaunchKernelGGL(chroma_summary_kernel, dim3(256), dim3(1024), kSumLds, s, t, ct);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(chroma_block_kernel<false>, dim3(4096 / kBlocksPerGroup), dim3(64 * kBlocksPerGroup), 0, s, ct);
+  hipLaunchKernelGGL(chroma_block_kernel<true>, dim3(4096 / kBlocksPerGroup), dim3(64 * kBlocksPerGroup), 0, s, ct);
   return hipGetLastError();
 }
 

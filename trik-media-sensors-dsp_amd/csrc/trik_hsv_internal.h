@@ -90,7 +90,7 @@ struct alignas(16) ChromaTables {
   uint32_t summary_drop[65536];
   uint16_t first_nz[65536];
   unsigned long long best[4096];
-  uint32_t block_cost[4096];  // the palette pass's cost per block (summed by chroma_cost_kernel)
+  uint32_t block_cost[4096];  // the palette pass's cost per block (summed by its last workgroup)
   uint32_t pair_hist[256];
   uint32_t palette[2 * kChromaPalette];
   uint8_t palette_of[256];
@@ -106,6 +106,10 @@ struct alignas(16) ChromaTables {
 
 PackedRange pack_range(const TRIK_VIDTRANSCODE_CV_InArgsAlg& r);
 void compile_tables(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTables* out);
+// compile_tables in two parts: the head (LUTs, per-value H/S/V tests) first,
+// then the sat/val table (which reads the head's lut255)
+void compile_tables_head(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTables* out);
+void compile_tables_sv(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTables* out);
 void compile_stripe_tables(const RangeTables& base, int n, StripeTables* out);
 // Which tests of detectHsvPixel (WSEQ:171-179) a group of n compiled ranges
 // needs: kDetectFull; kDetectSV when each accepts every hue value; kDetectV
@@ -249,6 +253,16 @@ bool chroma_fused_ok(const KernelArgs& a);
 int launch_chroma(const KernelArgs& a, const ChromaTables* ct, bool write_masks, hipStream_t s);
 // Sets the calling thread's trik_hsv_last_error() message; returns code.
 int32_t set_error(int32_t code, const std::string& msg);
+// The packed ranges of up to kTableGroups groups of <= 4 (kernel argument).
+constexpr int kTableGroups = 16;
+struct TableBuildArgs {
+  uint32_t from[kTableGroups * 4], to[kTableGroups * 4], expect[kTableGroups * 4];
+  int32_t n_ranges;  // over all groups
+};
+// compile_tables + compile_stripe_tables on the device from the packed ranges
+// alone (groups <= kTableGroups): no host-built table crosses PCIe.
+int launch_compile_tables(const TableBuildArgs& args, int groups, RangeTables* d_tables, StripeTables* d_stripe,
+                          hipStream_t s);
 int launch_totals(int n_frames, int n_ranges, const TrikHsvTargetSums* sums, TrikHsvTargetSums* totals,
                   hipStream_t s);
 int launch_targets(const TrikHsvFrameBatch& b, int n_ranges, const TrikHsvTargetSums* sums,

@@ -325,6 +325,61 @@ int launch_reduce(const KernelArgs& a, bool write_masks, hipStream_t s) {
                      : dispatch_aligned<TRIK_HSV_LAYOUT_OV7670, false>(a, s);
 }
 
+// One workgroup of 256 per (group, mx) row: the range tables of
+// compile_tables (trik_hsv_tables.cpp) and the stripe kernel's tables of
+// compile_stripe_tables, from the packed ranges (WSEQ:425-445) -- the same
+// per-range tests: hue by the wrap-aware "outside" pattern, S and V by their
+// byte intervals, sv[mx][mn] when mn <= mx, V = mx in [fv, tv] and
+// S = (LUT255[mx] (mx - mn)) >> 8 in [fs, ts] (WSEQ:389-407).  Row mx = 0 of
+// each group also writes the per-value tables.
+__global__ __launch_bounds__(256) void compile_tables_kernel(TableBuildArgs a, RangeTables* tabs, StripeTables* strs) {
+  const int g = (int)blockIdx.y, mx = (int)blockIdx.x, mn = (int)threadIdx.x;
+  const int n0 = 4 * g, cnt = a.n_ranges - n0 < 4 ? a.n_ranges - n0 : 4;
+  RangeTables& t = tabs[g];
+  StripeTables& st = strs[g];
+  auto outside = [](uint32_t x, uint32_t lo, uint32_t hi) { return x < lo || x > hi; };
+  const uint32_t l255 = mx ? (255u * 256u) / (uint32_t)mx : 0u;
+  uint32_t sv = 0;
+  for (int r = 0; r < cnt; ++r) {
+    const uint32_t from = a.from[n0 + r], to = a.to[n0 + r];
+    const uint32_t fs = (from >> 8) & 0xFFu, ts = (to >> 8) & 0xFFu;
+    const uint32_t fv = (from >> 16) & 0xFFu, tv = (to >> 16) & 0xFFu;
+    const uint32_t S = (l255 * (uint32_t)(mx - mn)) >> 8;
+    if (mn <= mx && !outside((uint32_t)mx, fv, tv) && !outside(S, fs, ts)) sv |= 1u << r;
+  }
+  t.sv[mx * 256 + mn] = (uint8_t)sv;
+  st.sv[mx * kSvStride + mn] = (uint8_t)sv;
+  if (mn < kSvStride - 256) st.sv[mx * kSvStride + 256 + mn] = 0;
+  if (mx == 0) {  // the per-value tables, index i = mn
+    const uint32_t i = (uint32_t)mn;
+    uint8_t hue = 0, sm = 0, vm = 0;
+    for (int r = 0; r < cnt; ++r) {
+      const uint32_t from = a.from[n0 + r], to = a.to[n0 + r];
+      const uint8_t bit = (uint8_t)(1u << r);
+      if ((outside(i, from & 0xFFu, to & 0xFFu) ? 1u : 0u) == (a.expect[n0 + r] & 1u)) hue |= bit;
+      if (!outside(i, (from >> 8) & 0xFFu, (to >> 8) & 0xFFu)) sm |= bit;
+      if (!outside(i, (from >> 16) & 0xFFu, (to >> 16) & 0xFFu)) vm |= bit;
+    }
+    const uint16_t l43 = i ? (uint16_t)((43u * 256u) / i) : (uint16_t)0;
+    t.hue[i] = hue;
+    t.smask[i] = sm;
+    t.vmask[i] = vm;
+    t.lut43[i] = l43;
+    t.lut255[i] = i ? (uint16_t)((255u * 256u) / i) : (uint16_t)0;
+    uint32_t spread = 0;
+    for (int r = 0; r < cnt; ++r) spread |= ((uint32_t)(hue >> r) & 1u) << (8 * r);
+    for (int c = 0; c < kHueCopies; ++c) st.hue[i * kHueCopies + c] = spread;
+    for (int c = 0; c < kM43Copies; ++c) st.m43[i * kM43Copies + c] = l43;
+  }
+}
+
+int launch_compile_tables(const TableBuildArgs& args, int groups, RangeTables* d_tables, StripeTables* d_stripe,
+                          hipStream_t s) {
+  if (groups <= 0 || groups > kTableGroups) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(compile_tables_kernel, dim3(256, groups), dim3(256), 0, s, args, d_tables, d_stripe);
+  return hipGetLastError();
+}
+
 int launch_targets(const TrikHsvFrameBatch& b, int n_ranges, const TrikHsvTargetSums* sums,
                    TrikHsvTarget* targets, hipStream_t s) {
   const int n = b.n_frames * n_ranges;

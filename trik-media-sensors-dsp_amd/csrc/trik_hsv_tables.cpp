@@ -40,15 +40,18 @@ PackedRange pack_range(const TRIK_VIDTRANSCODE_CV_InArgsAlg& r) {  // WSEQ:425-4
 
 static inline bool outside(uint32_t x, uint32_t lo, uint32_t hi) { return x < lo || x > hi; }
 
-void compile_tables(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTables* out) {
-  memset(out, 0, sizeof(*out));
+// Everything but the sat/val table: the LUTs and the per-value H, S, V tests
+// (what the chroma-run builder and kernel read).
+void compile_tables_head(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTables* out) {
+  memset(out->hue, 0, sizeof(out->hue));
+  memset(out->smask, 0, sizeof(out->smask));
+  memset(out->vmask, 0, sizeof(out->vmask));
   out->lut43[0] = 0;
   out->lut255[0] = 0;
   for (uint32_t i = 1; i < 256; ++i) {  // WSEQ:400-406
     out->lut43[i] = (uint16_t)((43u * 256u) / i);
     out->lut255[i] = (uint16_t)((255u * 256u) / i);
   }
-  const uint16_t* lut255 = out->lut255;
   for (int t = 0; t < n; ++t) {
     const PackedRange p = pack_range(ranges[t]);
     const uint8_t bit = (uint8_t)(1u << t);
@@ -61,10 +64,21 @@ void compile_tables(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTa
       if (!outside(x, fs, ts)) out->smask[x] |= bit;
       if (!outside(x, fv, tv)) out->vmask[x] |= bit;
     }
-    // S = (LUT255[mx] * d) >> 8 with d = mx - mn does not fall as d grows, so
-    // the d with fs <= S <= ts form one interval [d_lo, d_hi]: solved per mx
-    // instead of testing every (mx, mn) (a new range set is compiled on the
-    // host before its batch is enqueued)
+  }
+}
+
+// The sat/val table sv[mx * 256 + mn] (compile_tables_head first: it reads
+// lut255).  S = (LUT255[mx] * d) >> 8 with d = mx - mn does not fall as d
+// grows, so the d with fs <= S <= ts form one interval [d_lo, d_hi]: solved
+// per mx instead of testing every (mx, mn).
+void compile_tables_sv(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTables* out) {
+  memset(out->sv, 0, sizeof(out->sv));
+  const uint16_t* lut255 = out->lut255;
+  for (int t = 0; t < n; ++t) {
+    const PackedRange p = pack_range(ranges[t]);
+    const uint8_t bit = (uint8_t)(1u << t);
+    const uint32_t fs = (p.from >> 8) & 0xFF, ts = (p.to >> 8) & 0xFF;
+    const uint32_t fv = (p.from >> 16) & 0xFF, tv = (p.to >> 16) & 0xFF;
     for (uint32_t mx = fv; mx <= tv && mx < 256; ++mx) {
       const uint32_t L = lut255[mx];
       uint32_t d_lo, d_hi;
@@ -81,6 +95,11 @@ void compile_tables(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTa
       for (uint32_t d = d_lo; d <= d_hi; ++d) row[mx - d] |= bit;
     }
   }
+}
+
+void compile_tables(const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int n, RangeTables* out) {
+  compile_tables_head(ranges, n, out);
+  compile_tables_sv(ranges, n, out);
 }
 
 void compile_stripe_tables(const RangeTables& base, int n, StripeTables* out) {
