@@ -245,14 +245,18 @@ __device__ __forceinline__ void stage_exact_tables(const RangeTables* t, int tid
 // One workgroup of 1024 per V: the exact T-bit mask of every (Y, U) -- the
 // 256 chromas' profiles, two Y per YUYV word through exact_mask (the stripe
 // kernel's arithmetic on LDS tables, held to the oracle on all 2^24 triples)
-// into LDS -- then one thread per chroma summarises its profile's runs with
-// the trailing zero run removed:
+// into LDS -- then each chroma's profile summarised as its runs with the
+// trailing zero run removed:
 //   bits 0-1 number of runs (3 = more than two), 4-7 v1, 8-11 v2,
 //   12-20 end of run 1, 21-29 end of run 2 (two runs) or of the last nonzero
 //   run (more than two).
+// The walk is split in four 64-Y segments per chroma (one thread each: its
+// first and last mask, its value changes -- the first three with their Y --
+// and its last nonzero Y), which one thread per chroma then joins.
 constexpr uint32_t kSumStride = 260;  // profile rows, padded against bank conflicts
 constexpr uint32_t kSumProf = 16384;  // [256][kSumStride] u8, after the exact tables
-constexpr uint32_t kSumLds = kSumProf + 256 * kSumStride;
+constexpr uint32_t kSumSeg = kSumProf + 256 * kSumStride;  // [4][256] segment records of 8 u32
+constexpr uint32_t kSumLds = kSumSeg + 4 * 256 * 32;
 static_assert(kLdsVal + 256 <= kSumProf && kSumLds <= 160 * 1024, "summary LDS image");
 __global__ __launch_bounds__(1024) void chroma_summary_kernel(const RangeTables* t, ChromaTables* ct) {
   const uint32_t V = blockIdx.x, tid = threadIdx.x;
@@ -262,38 +266,86 @@ __global__ __launch_bounds__(1024) void chroma_summary_kernel(const RangeTables*
     ct->flagged_words = 0ull;
   }
   __syncthreads();
-  {  // lane U of a wave, 32 Y pairs per thread
-    const uint32_t U = tid & 255u, j0 = (tid >> 8) * 32u;
-    const uint32_t row = kSumProf + U * kSumStride;
-    for (uint32_t j = j0; j < j0 + 32u; ++j) {
-      const uint32_t w = (2u * j) | (U << 8) | ((2u * j + 1u) << 16) | (V << 24);
-      *(lds16_t)(uintptr_t)(row + 2u * j) = (uint16_t)(exact_mask<0>(w) | (exact_mask<1>(w) << 8));
+  const uint32_t U = tid & 255u, seg = tid >> 8;  // a wave: 64 chromas, one segment
+  const uint32_t row = kSumProf + U * kSumStride;
+  for (uint32_t j = seg * 32u; j < seg * 32u + 32u; ++j) {
+    const uint32_t w = (2u * j) | (U << 8) | ((2u * j + 1u) << 16) | (V << 24);
+    *(lds16_t)(uintptr_t)(row + 2u * j) = (uint16_t)(exact_mask<0>(w) | (exact_mask<1>(w) << 8));
+  }
+  __syncthreads();
+  {  // this segment: Y in [64 seg, 64 seg + 64)
+    const uint32_t y0 = 64u * seg;
+    uint32_t q = *(lds32_t)(uintptr_t)(row + y0);
+    const uint32_t first = q & 0xFFu;
+    // (the first three changes in three registers by selects: an array
+    // indexed by a per-lane count would live in scratch memory)
+    uint32_t prev = first, c = 0, cz = 0, ev0 = 0, ev1 = 0, ev2 = 0;  // ev: Y | value << 16
+    int lnz = first ? (int)y0 : -1;
+    for (uint32_t k = 1; k < 64; ++k) {
+      if ((k & 3u) == 0) q = *(lds32_t)(uintptr_t)(row + y0 + k);
+      const uint32_t m = (q >> (8u * (k & 3u))) & 0xFFu;
+      const uint32_t e = (y0 + k) | (m << 16);
+      const bool chg = m != prev;
+      ev0 = chg && c == 0 ? e : ev0;
+      ev1 = chg && c == 1 ? e : ev1;
+      ev2 = chg && c == 2 ? e : ev2;
+      c += chg ? 1u : 0u;
+      prev = m;
+      lnz = m ? (int)(y0 + k) : lnz;
+      cz = m ? c : cz;
     }
+    const uint32_t ne = c < 3 ? c : 3u;
+    const uint32_t ev[3] = {ev0, ev1, ev2};
+    const uint32_t rec = kSumSeg + (seg * 256u + U) * 32u;
+    *(lds32_t)(uintptr_t)(rec + 0) = first | (prev << 8) | (ne << 16);
+    *(lds32_t)(uintptr_t)(rec + 4) = c;
+    *(lds32_t)(uintptr_t)(rec + 8) = cz;
+    *(lds32_t)(uintptr_t)(rec + 12) = (uint32_t)lnz;
+    *(lds32_t)(uintptr_t)(rec + 16) = ev[0];
+    *(lds32_t)(uintptr_t)(rec + 20) = ev[1];
+    *(lds32_t)(uintptr_t)(rec + 24) = ev[2];
   }
   __syncthreads();
   if (tid >= 256u) return;
-  const uint32_t U = tid;
-  const uint32_t row = kSumProf + U * kSumStride;
+  // the join: the run sequence is the segments' changes in order, plus a
+  // change at a segment's first Y when its first mask differs from the last
+  // mask before it
   const uint32_t c = U | (V << 8);
-  int nruns = 0;            // runs so far, including the current one
-  uint32_t vals[3] = {0, 0, 0};
-  int ends[3] = {0, 0, 0};  // exclusive end of each run
-  uint32_t cur = 0xFFu;
+  uint32_t v0 = 0, v1 = 0, v2 = 0;   // run values (selects, not a dynamically indexed array)
+  int e0 = 256, e1 = 256, e2 = 256;  // exclusive end of runs 0..2 (the next run's first Y)
+  int n_ev = 0;                      // changes so far (run k starts at the k-th change)
   int last_nz_run = -1, last_nz_end = 0;
-  for (int Y4 = 0; Y4 < 256; Y4 += 4) {
-    const uint32_t q = *(lds32_t)(uintptr_t)(row + (uint32_t)Y4);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int Y = Y4 + k;
-      const uint32_t m = (q >> (8 * k)) & 0xFFu;
-      if (m != cur) {
-        if (nruns < 3) vals[nruns] = m;
-        ++nruns;
-        cur = m;
-      }
-      if (nruns <= 3) ends[nruns - 1] = Y + 1;
-      if (m) { last_nz_run = nruns - 1; last_nz_end = Y + 1; }
+  uint32_t cur = 0;
+  for (uint32_t sg = 0; sg < 4; ++sg) {
+    const uint32_t rec = kSumSeg + (sg * 256u + U) * 32u;
+    const uint32_t h = *(lds32_t)(uintptr_t)(rec + 0);
+    const uint32_t first = h & 0xFFu, last = (h >> 8) & 0xFFu, ne = h >> 16;
+    const int cnt = (int)*(lds32_t)(uintptr_t)(rec + 4), cz = (int)*(lds32_t)(uintptr_t)(rec + 8);
+    const int lnz = (int)*(lds32_t)(uintptr_t)(rec + 12);
+    auto change = [&](int y, uint32_t v) {
+      e0 = n_ev == 0 ? y : e0;
+      e1 = n_ev == 1 ? y : e1;
+      e2 = n_ev == 2 ? y : e2;
+      v1 = n_ev == 0 ? v : v1;
+      v2 = n_ev == 1 ? v : v2;
+      ++n_ev;
+    };
+    if (sg == 0) {
+      v0 = first;
+    } else if (first != cur) {
+      change((int)(64u * sg), first);
     }
+    const int before = n_ev;  // changes before this segment's own
+    for (uint32_t i = 0; i < 3; ++i) {
+      const uint32_t e = *(lds32_t)(uintptr_t)(rec + 16 + 4 * i);
+      if (i < ne && n_ev < 3) change((int)(e & 0xFFFFu), e >> 16);
+    }
+    n_ev = before + cnt;
+    if (lnz >= 0) {
+      last_nz_run = before + cz;
+      last_nz_end = lnz + 1;
+    }
+    cur = last;
   }
   // runs up to and including the last nonzero one
   const int n = last_nz_run + 1;  // 0: all zero
@@ -305,13 +357,14 @@ __global__ __launch_bounds__(1024) void chroma_summary_kernel(const RangeTables*
     return (uint32_t)(nn > 2 ? 3 : nn) | (v1 << 4) | ((nn == 2 ? v2 : 0u) << 8) | ((uint32_t)a << 12) |
            ((uint32_t)ab << 21);
   };
-  const uint32_t sf = pack(n, vals[0], vals[1], ends[0]);
+  const uint32_t sf = pack(n, v0, v1, e0);
   ct->summary[c] = sf;
   // the profile from its first nonzero Y on: without a leading zero run the
   // same; with one, the runs after it (runs 1 and 2 become runs 0 and 1)
-  const bool lead0 = vals[0] == 0u && n > 0;
-  ct->summary_drop[c] = lead0 ? pack(n - 1, vals[1], vals[2], ends[1]) : sf;
-  ct->first_nz[c] = (uint16_t)(n == 0 ? 256 : (lead0 ? ends[0] : 0));
+  const bool lead0 = v0 == 0u && n > 0;
+  ct->summary_drop[c] = lead0 ? pack(n - 1, v1, v2, e1) : sf;
+  ct->first_nz[c] = (uint16_t)(n == 0 ? 256 : (lead0 ? e0 : 0));
+  (void)e2;
 }
 
 // The run descriptor of one chroma under block masks (M1, M2).  With
