@@ -122,6 +122,10 @@ def lib():
                                            C.POINTER(BlobState), C.c_int, C.c_int, C.c_int, vp, i64,
                                            vp, vp, vp, vp, vp]
         L.trik_oracle_blob_run.restype = C.c_int
+        L.trik_oracle_wsgl_table.argtypes = [C.POINTER(Range), vp]
+        L.trik_oracle_wsgl_table.restype = None
+        L.trik_oracle_wsgl_run.argtypes = [vp, i64, C.c_int, C.c_int, C.c_int, C.POINTER(Range), vp, vp]
+        L.trik_oracle_wsgl_run.restype = C.c_int
         _lib = L
     return _lib
 
@@ -162,6 +166,25 @@ def pack_range(r):
     f, t, e = C.c_uint32(), C.c_uint32(), C.c_uint32()
     lib().trik_oracle_pack_range(C.byref(Range(*r)), C.byref(f), C.byref(t), C.byref(e))
     return f.value, t.value, e.value
+
+
+def wsgl_table(r) -> np.ndarray:
+    """The single-pass detector (WSGL) on every (Y, U, V): 2^24 bytes, bit 0 /
+    bit 1 = the word's first / second pixel with that luma."""
+    out = np.zeros(1 << 24, np.uint8)
+    lib().trik_oracle_wsgl_table(C.byref(Range(*r)), _ptr(out))
+    return out
+
+
+def wsgl_run(frame_u8: np.ndarray, width, height, line_length, r):
+    """One packed-YUYV frame through WSGL's run(): (sums[3] int64, (x, y, size))."""
+    fr = np.ascontiguousarray(frame_u8, dtype=np.uint8)
+    sums = np.zeros(3, np.int64)
+    tg = np.zeros(3, np.int32)
+    if not lib().trik_oracle_wsgl_run(_ptr(fr), fr.size, width, height, line_length, C.byref(Range(*r)),
+                                      _ptr(sums), _ptr(tg)):
+        raise ValueError("WSGL run() would return false")
+    return sums, tuple(int(v) for v in tg)
 
 
 def frame_bytes(width, height, line_length, layout) -> int:

@@ -122,6 +122,17 @@ int      trik_cpu_batch(const uint8_t* frames, int64_t frame_stride, int n_frame
                         const trik_oracle_range* ranges, int n_ranges, int64_t* sums,
                         int n_threads);
 
+/* The single-pass webcam detector (WSGL, trik_oracle_wsgl.c): a second
+ * reference text restated for cross-checking the WSEQ restatement above.
+ * table: out[Y | U << 8 | V << 16] bit 0 / bit 1 = detection of the first /
+ * second pixel of a YUYV word with that luma (2^24 bytes).  run: one packed
+ * YUYV frame, one range: sums {N, sum x, sum y} and target {x, y, size};
+ * returns 0 when WSGL's run() would return false, else 1. */
+void     trik_oracle_wsgl_table(const trik_oracle_range* range, uint8_t* out);
+int      trik_oracle_wsgl_run(const uint8_t* frame, int64_t frame_size, int width, int height,
+                              int line_length, const trik_oracle_range* range, int64_t sums[3],
+                              int32_t target[3]);
+
 /* Synthetic frame generators shared bit-for-bit with the device generator
  * (synth kernels in trik-media-sensors-dsp_amd/csrc/trik_hsv_kernels.hip).
  * kind 0 = uniform random bytes, kind 1 = scene (gradients + 6 discs). */
