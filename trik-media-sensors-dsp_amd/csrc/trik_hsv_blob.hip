@@ -18,7 +18,10 @@
 //      up-row minima -- one segmented min-scan per row across the wave;
 //    * statistics: every non-opening set metapixel adds (c, r, 1) to its
 //      label (CLU:91-95; the opening one is not counted, CLU:98-112), with
-//      one atomic per run of equal labels in a lane;
+//      one atomic per run of equal labels in a lane -- one 64-bit atomic of
+//      the packed (size, sum x, sum y) when the frame's maxima fit 63 bits
+//      (VGA: 15 + 21 + 21), else three 32-bit ones;
+//    * the bitmap row r + 1 is loaded while row r is labelled;
 //    * equivalences: eq[a] = eq[L] for each non-zero neighbour a (equal to
 //      the reference's conditional form, CLU:92-96), in raster order; only
 //      metapixels with a neighbour label other than L can change anything,
@@ -190,30 +193,63 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
     meta = reinterpret_cast<const uint8_t*>(dst);
     __syncthreads();
   }
-  // own[3k + {0,1,2}] = x, y, size (zeroed by the launcher); fin: folded
+  // own statistics (zeroed by the launcher): packed, own64[k] = size |
+  // x << pack_sx | y << pack_sy; else own[3k + {0,1,2}] = x, y, size.
+  // fin: folded, [3k + {0,1,2}] = x, y, size
   int32_t* own = a.stats + (int64_t)f * 3 * ml;
+  unsigned long long* own64 = reinterpret_cast<unsigned long long*>(a.stats) + (int64_t)f * ml;
   int32_t* fin = a.stats + ((int64_t)a.n_frames + f) * 3 * ml;
+  const bool packed = a.pack_sx != 0;
+  auto add_own = [&](uint32_t L, int32_t x, int32_t y, int32_t n) {
+    if (packed) {
+      atomicAdd(own64 + L, (unsigned long long)(uint32_t)n | ((unsigned long long)(uint32_t)x << a.pack_sx) |
+                               ((unsigned long long)(uint32_t)y << a.pack_sy));
+    } else {
+      atomicAdd(&own[3 * L], x);
+      atomicAdd(&own[3 * L + 1], y);
+      atomicAdd(&own[3 * L + 2], n);
+    }
+  };
+  auto get_own = [&](int k, int32_t& x, int32_t& y, int32_t& n) {
+    if (packed) {
+      const unsigned long long v = own64[k];
+      n = (int32_t)(v & ((1ull << a.pack_sx) - 1ull));
+      x = (int32_t)((v >> a.pack_sx) & ((1ull << (a.pack_sy - a.pack_sx)) - 1ull));
+      y = (int32_t)(v >> a.pack_sy);
+    } else {
+      x = own[3 * k];
+      y = own[3 * k + 1];
+      n = own[3 * k + 2];
+    }
+  };
   uint16_t* labels = a.labels ? a.labels + (int64_t)f * bw * bh : nullptr;
 
   const int K = (bw + 63) / 64;
   const int c0 = lane * K;
-  uint32_t prv[KMAX], cur[KMAX], dd[KMAX], up[KMAX];
+  uint32_t prv[KMAX], cur[KMAX], dd[KMAX], up[KMAX], nx[KMAX];
 #pragma unroll
   for (int j = 0; j < KMAX; ++j) prv[j] = 0;
   if (lane == 0) eq[0] = 0;
+  // this lane's columns of bitmap row r (loaded a row ahead: the loads of row
+  // r + 1 are in flight while row r is labelled)
+  auto load_row = [&](int r, uint32_t (&o)[KMAX]) {
+    const uint8_t* mrow = meta + (int64_t)r * bw;
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) o[j] = (j < K && c0 + j < bw) ? (uint32_t)mrow[c0 + j] : 0u;
+  };
+  if (bh > 0) load_row(0, nx);
   int next = 1;  // next new label (wave-uniform)
   for (int r = 0; r < bh; ++r) {
-    const uint8_t* mrow = meta + (int64_t)r * bw;
     uint32_t prev_last = 0, d_last = 0;
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) {
-      const int c = c0 + j;
-      dd[j] = (j < K && c < bw) ? (uint32_t)mrow[c] : 0u;
+      dd[j] = nx[j];
       if (j == K - 1) {
         prev_last = prv[j];
         d_last = dd[j];
       }
     }
+    if (r + 1 < bh) load_row(r + 1, nx);
     // the neighbours' boundary columns (CLU:70-84 reads c-1 and c+1)
     uint32_t l_prev = __shfl_up(prev_last, 1, 64), l_d = __shfl_up(d_last, 1, 64);
     uint32_t r_prev = __shfl_down(prv[0], 1, 64);
@@ -300,11 +336,7 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
         const uint32_t L = cur[j];
         if (L && !((seeds >> j) & 1u)) {
           if (L != acc_l) {
-            if (an) {
-              atomicAdd(&own[3 * acc_l], ax);
-              atomicAdd(&own[3 * acc_l + 1], ay);
-              atomicAdd(&own[3 * acc_l + 2], an);
-            }
+            if (an) add_own(acc_l, ax, ay, an);
             acc_l = L;
             ax = ay = an = 0;
           }
@@ -319,11 +351,7 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
         }
         if (labels && j < K && c0 + j < bw) labels[(int64_t)r * bw + c0 + j] = (uint16_t)L;
       }
-      if (an) {
-        atomicAdd(&own[3 * acc_l], ax);
-        atomicAdd(&own[3 * acc_l + 1], ay);
-        atomicAdd(&own[3 * acc_l + 2], an);
-      }
+      if (an) add_own(acc_l, ax, ay, an);
     }
     // equivalence events in raster order: lane by lane, each lane in column
     // order (CLU:92-96 as eq[a] = eq[L] for every non-zero neighbour a)
@@ -358,18 +386,22 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
       fin[0] = fin[1] = fin[2] = 0;
       continue;
     }
-    fin[3 * k] = own[3 * k];
-    fin[3 * k + 1] = own[3 * k + 1];
-    fin[3 * k + 2] = eq[k] == k ? own[3 * k + 2] : 0;
+    int32_t x, y, sz;
+    get_own(k, x, y, sz);
+    fin[3 * k] = x;
+    fin[3 * k + 1] = y;
+    fin[3 * k + 2] = eq[k] == k ? sz : 0;
   }
   __threadfence();
   __syncthreads();
   for (int k = lane + 0; k < n; k += 64) {
     const int e = eq[k];
     if (k != 0 && e != k) {
-      atomicAdd(&fin[3 * e], own[3 * k]);
-      atomicAdd(&fin[3 * e + 1], own[3 * k + 1]);
-      atomicAdd(&fin[3 * e + 2], own[3 * k + 2]);
+      int32_t x, y, sz;
+      get_own(k, x, y, sz);
+      atomicAdd(&fin[3 * e], x);
+      atomicAdd(&fin[3 * e + 1], y);
+      atomicAdd(&fin[3 * e + 2], sz);
     }
   }
   __threadfence();
@@ -435,8 +467,26 @@ int launch_blob(const BlobArgs& a, hipStream_t s) {
   if (a.n_frames <= 0 || a.width <= 0 || a.height <= 0) return hipSuccess;
   const int bw = a.width >> 2, bh = a.height >> 2;
   if (bw > 64 * 32) return hipErrorInvalidValue;  // events mask: 32 columns per lane
-  // own statistics start at zero ([n][max_labels][3] at the front of stats)
-  hipError_t z = hipMemsetAsync(a.stats, 0, sizeof(int32_t) * 3 * (size_t)a.max_labels * (size_t)a.n_frames, s);
+  // own statistics: one packed u64 per label when the frame's maxima (size
+  // <= bw*bh, sum x <= bh*bw(bw-1)/2, sum y <= bw*bh(bh-1)/2) fit 63 bits
+  BlobArgs b = a;
+  {
+    auto bits = [](uint64_t v) {
+      int n = 0;
+      while (n < 64 && (v >> n)) ++n;
+      return n;
+    };
+    const uint64_t w = (uint64_t)bw, h = (uint64_t)bh;
+    const int bn = bits(w * h), bx = bits(h * w * (w ? w - 1 : 0) / 2), by = bits(w * h * (h ? h - 1 : 0) / 2);
+    b.pack_sx = b.pack_sy = 0;
+    if (bn > 0 && bn + bx + by <= 63) {
+      b.pack_sx = bn;
+      b.pack_sy = bn + bx;
+    }
+  }
+  // own statistics start at zero (at the front of stats)
+  const size_t own_bytes = (b.pack_sx ? sizeof(uint64_t) : 3 * sizeof(int32_t)) * (size_t)a.max_labels * (size_t)a.n_frames;
+  hipError_t z = hipMemsetAsync(a.stats, 0, own_bytes, s);
   if (z != hipSuccess) return z;
   const int64_t total = (int64_t)a.n_frames * bw * bh;
   if (total >= (1ll << 31) || !a.tables) return hipErrorInvalidValue;
@@ -458,7 +508,6 @@ int launch_blob(const BlobArgs& a, hipStream_t s) {
   }
   size_t lds = sizeof(uint16_t) * (size_t)((a.max_labels + 1) & ~1);
   if (lds > 64 * 1024) return hipErrorInvalidValue;
-  BlobArgs b = a;
   // the frame's bitmap staged in LDS when it fits and the batch is small
   // (latency); large batches read it from L2 instead, so that the eq table
   // alone bounds the residency (VGA: 16 frames per CU instead of 5; 4096

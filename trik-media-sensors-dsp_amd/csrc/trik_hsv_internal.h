@@ -299,6 +299,9 @@ struct BlobArgs {
   int32_t* n_labels;         // optional [n]
   int32_t meta_lds = 0;      // set by launch_blob: the bitmap staged in LDS
   int32_t meta_ready = 0;    // the bitmap is already written (launch_blob_meta_chroma)
+  // set by launch_blob: the own statistics as one packed u64 per label,
+  // size | sum_x << pack_sx | sum_y << pack_sy (0: three int32 per label)
+  int32_t pack_sx = 0, pack_sy = 0;
   // gate of the bitmap kernel (as KernelArgs::gate): the chroma-run bitmap and
   // the stripe-arithmetic bitmap are both launched, one of them runs
   const unsigned long long* gate = nullptr;
