@@ -214,6 +214,25 @@ def test_chroma_exhaustive_adversarial(torch_dev, detector, oracle_mod, chroma, 
     assert sums[0].cpu().numpy().tolist() == sums_from_mask(want, len(ranges)).tolist()
 
 
+# hue-bounded S/V bands (scripts/adversarial_ranges.py "hue0-30 S50-60" and
+# mixed sets): most chromas stay runs or windows, the share stays low
+HUE_BANDS = [(0, 30, 50, 60, 0, 100), (60, 120, 30, 60, 0, 100), (200, 260, 30, 40, 20, 100),
+             (330, 20, 50, 60, 30, 100)]
+
+
+@pytest.mark.parametrize("ranges", [HUE_BANDS[:1], HUE_BANDS], ids=["hue0_30_s50_60", "hue_bands4"])
+def test_chroma_exhaustive_hue_bands(torch_dev, detector, oracle_mod, chroma, ranges):
+    """Every (Y,U,V) triple through hue-bounded S/V band sets on the chroma kernel."""
+    torch = torch_dev
+    frame, w, h, ll = exhaustive_yuyv_frame()
+    _, want = oracle_mod.frame(frame, w, h, ll, LAYOUT_YUYV, ranges, want_mask=True)
+    masks, sums = detector.batch_masks(_to_dev(torch, frame), w, h, ll, LAYOUT_YUYV, ranges)
+    assert chroma.last_hot_kernel() == HOT_CHROMA
+    got = masks[0].cpu().numpy()
+    assert np.array_equal(got, want), f"{np.count_nonzero(got != want)} pixels differ"
+    assert sums[0].cpu().numpy().tolist() == sums_from_mask(want, len(ranges)).tolist()
+
+
 def test_auto_share_guard(torch_dev, hsv, oracle_mod):
     """AUTO runs the chroma kernel for the bench ranges (share ~2.9 %) and the
     stripe kernel for a range set whose exact-path share is above
