@@ -1,7 +1,8 @@
 """A/B timing of the multi-blob pipeline (trik_hsv_blob_batch, 4096 ov7670 VGA
-frames) across library variants (development only; GPU box).
+frames) or of autoDetectHsv (--what range: trik_hsv_batch_auto_range, 4096
+YUYV VGA frames) across library variants (development only; GPU box).
 
-usage: python scripts/blob_ab.py [--frames N] [--reps R] lib1 [lib2 ...]
+usage: python scripts/blob_ab.py [--what blob|range] [--frames N] [--reps R] lib1 [lib2 ...]
   libs: paths to libtrik_hsv.so variants (e.g. trik-media-sensors-dsp_amd/ab/x/libtrik_hsv.so)
 
 Each variant runs in its own process on a private copy of the host package
@@ -52,8 +53,41 @@ print(json.dumps(res))
 """
 
 
+CHILD_RANGE = r"""
+import hashlib, json, sys
+import torch
+import trik_hsv
+F, reps = int(sys.argv[1]), int(sys.argv[2])
+W, H, LL = 640, 480, 1280
+dev = torch.empty(F * H * LL, dtype=torch.uint8, device="cuda")
+s = torch.cuda.current_stream()
+res = {}
+for kind in (0, 1):
+    if kind == 1:
+        trik_hsv.synth(dev, W, H, LL, trik_hsv.LAYOUT_YUYV, 1, 0x7A1C)
+    else:
+        trik_hsv.synth(dev, W, H, LL, trik_hsv.LAYOUT_YUYV, 0, 0x7A1C)
+    out = trik_hsv.batch_auto_range(dev, W, H, LL, trik_hsv.LAYOUT_YUYV, stream=s)
+    torch.cuda.synchronize()
+    digest = hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()[:16]
+    t = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        for _ in range(5):
+            trik_hsv.batch_auto_range(dev, W, H, LL, trik_hsv.LAYOUT_YUYV, stream=s)
+        b.record(s)
+        torch.cuda.synchronize()
+        t.append(a.elapsed_time(b) / 5)
+    t.sort()
+    res[kind] = {"ms": round(t[len(t) // 2], 4), "min": round(t[0], 4), "digest": digest, "labels_mean": 0}
+print(json.dumps(res))
+"""
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--what", choices=["blob", "range"], default="blob")
     ap.add_argument("--frames", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=9)
     ap.add_argument("libs", nargs="+")
@@ -64,7 +98,7 @@ def main():
             shutil.copytree(PKG, os.path.join(d, "trik_hsv"), ignore=shutil.ignore_patterns("*.so", "__pycache__"))
             shutil.copy(lib, os.path.join(d, "trik_hsv", "libtrik_hsv.so"))
             env = dict(os.environ, PYTHONPATH=d)
-            r = subprocess.run([sys.executable, "-c", CHILD, str(a.frames), str(a.reps)], env=env,
+            r = subprocess.run([sys.executable, "-c", CHILD if a.what == "blob" else CHILD_RANGE, str(a.frames), str(a.reps)], env=env,
                                capture_output=True, text=True, timeout=300)
             if r.returncode:
                 print(lib, "FAILED", r.stderr[-2000:], flush=True)

@@ -4,12 +4,15 @@
 # objects of build/ -> trik-media-sensors-dsp_amd/ab/NAME/libtrik_hsv.so.
 #   bash scripts/build_variant.sh NAME FILE 'pattern=>replacement' ...
 # (the shipped sources carry no attribution switches; the variants live here)
+# REV=<git rev> takes csrc/FILE as of that revision instead of the work tree.
 set -eu
 cd "$(dirname "$0")/../trik-media-sensors-dsp_amd"
 make -s -C csrc >/dev/null
 N="$1"; F="$2"; shift 2
 mkdir -p "ab/$N"
-python3 - "csrc/$F" "ab/$N/$F" "$@" <<'PY'
+SRC="csrc/$F"
+if [ -n "${REV:-}" ]; then git show "$REV:trik-media-sensors-dsp_amd/csrc/$F" > "ab/$N/$F.rev"; SRC="ab/$N/$F.rev"; fi
+python3 - "$SRC" "ab/$N/$F" "$@" <<'PY'
 import re, sys
 src, dst, subs = sys.argv[1], sys.argv[2], sys.argv[3:]
 s = open(src).read()

@@ -82,3 +82,26 @@ def test_auto_keeps_uniform_input_on_chroma(torch_dev, hsv):
     m = det.chroma_measured_share()
     assert abs(m - det.chroma_flagged_share()) < 0.005, m  # uniform bytes: measured = expected
     det.close()
+
+
+def test_auto_wide_rows_cold_set_counts_once(torch_dev, hsv, oracle_mod):
+    """Rows wider than the stripe kernel takes (9600 px: the chroma kernel's
+    wide mode, the stripe kernel's geometry refuses them) with a range set new
+    to the handle: the first batch is planned before the set's share is known
+    (gated launches); the sums must be counted once, equal to the oracle, on
+    the cold batch and the warm one (a gated chroma launch must not
+    be followed by an ungated partner)."""
+    torch = torch_dev
+    w, h, n = 9600, 64, 20  # 20 * 9600 * 64 px >= TRIK_HSV_CHROMA_MIN_PIXELS
+    ll = 2 * w
+    dev = torch.empty(n * h * ll, dtype=torch.uint8, device="cuda")
+    hsv.synth(dev, w, h, ll, LAYOUT_YUYV, 0, 0x7A1C)
+    want, _ = oracle_mod.batch(dev.cpu().numpy(), h * ll, n, w, h, ll, LAYOUT_YUYV, BENCH_RANGES, n_threads=16)
+    d = hsv.Detector()
+    try:
+        for _ in range(2):  # cold range set, then warm
+            sums, _ = d.process_batch(dev, w, h, ll, LAYOUT_YUYV, BENCH_RANGES)
+            torch.cuda.synchronize()
+            assert (sums.cpu().numpy() == want).all()
+    finally:
+        d.close()

@@ -973,12 +973,12 @@ int32_t grow(T*& p, size_t& cap, size_t bytes) {
 int32_t ensure_blob_scratch(TrikCvHandle* h, int n, int w, int hgt, hipStream_t s) {
   const size_t bw = (size_t)(w / 4), bh = (size_t)(hgt / 4), nn = (size_t)(n > 0 ? n : 1);
   const size_t ml = (size_t)blob_max_labels((int)bw, (int)bh);
-  if (nn * (bw * bh > 0 ? bw * bh : 1) > h->d_meta_cap || nn * 6 * ml * sizeof(int32_t) > h->d_blob_stats_cap ||
+  if (nn * (bw * bh > 0 ? bw * bh : 1) > h->d_meta_cap || nn * 3 * ml * sizeof(int32_t) > h->d_blob_stats_cap ||
       nn * 24 * sizeof(int32_t) > h->d_blob_top_cap || nn * 8 * sizeof(TrikHsvTarget) > h->d_blob_targets_cap)
     h->blob_users.wait_all();
   HIP_TRY(h->blob_users.order_after(s));
   int32_t r = grow(h->d_meta, h->d_meta_cap, nn * (bw * bh > 0 ? bw * bh : 1));
-  if (!r) r = grow(h->d_blob_stats, h->d_blob_stats_cap, nn * 6 * ml * sizeof(int32_t));
+  if (!r) r = grow(h->d_blob_stats, h->d_blob_stats_cap, nn * 3 * ml * sizeof(int32_t));
   if (!r) r = grow(h->d_blob_top, h->d_blob_top_cap, nn * 24 * sizeof(int32_t));
   if (!r) r = grow(h->d_blob_targets, h->d_blob_targets_cap, nn * 8 * sizeof(TrikHsvTarget));
   return r;

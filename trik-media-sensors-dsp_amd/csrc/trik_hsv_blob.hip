@@ -26,11 +26,14 @@
 //      the reference's conditional form, CLU:92-96), in raster order; only
 //      metapixels with a neighbour label other than L can change anything,
 //      and they are replayed serially by the owning lane, lane by lane;
-//    * postProcessing (CLU:115-127), order-free: label k ends with its own
-//      x, y (size only if eq[k] == k) plus the own sums of every j with
-//      eq[j] == k, j != k (eq[j] <= j, so j's sums are final when folded);
+//    * postProcessing (CLU:115-127), in place on the own statistics in
+//      ascending chunks of 64 labels: label k ends with its own x, y (size
+//      only if eq[k] == k) plus the own sums of every j with eq[j] == k,
+//      j != k (eq[j] <= j, so j's sums are its own when it is folded);
 //    * the 8 largest by size, ties by label (std::sort's order among equals
-//      is unspecified in the reference), and OSEQ:563-590's arithmetic.
+//      is unspecified in the reference) -- eight wave-maximum passes over
+//      the folded sizes, in LDS when they fit 16 bits -- and OSEQ:563-590's
+//      arithmetic.
 //  blob_overlay_kernel  guide lines, then a 3x3 red mark per kept target.
 #include <hip/hip_runtime.h>
 
@@ -150,6 +153,15 @@ __device__ __forceinline__ void wave_incl_segmin(uint32_t& b, uint32_t& m) {
   seg_step<0x143, 0xC>(b, m);
 }
 
+// lane l gets lane l - 1's v (lane 0: first); lane l gets lane l + 1's v
+// (lane 63: 0) -- DPP wave shifts (wave_shr:1 / wave_shl:1), no LDS permute
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t v, uint32_t first) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
+}
+
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -193,12 +205,11 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
     meta = reinterpret_cast<const uint8_t*>(dst);
     __syncthreads();
   }
-  // own statistics (zeroed by the launcher): packed, own64[k] = size |
-  // x << pack_sx | y << pack_sy; else own[3k + {0,1,2}] = x, y, size.
-  // fin: folded, [3k + {0,1,2}] = x, y, size
+  // own statistics (zeroed by the launcher; folded in place at the end):
+  // packed, own64[k] = size | x << pack_sx | y << pack_sy; else
+  // own[3k + {0,1,2}] = x, y, size
   int32_t* own = a.stats + (int64_t)f * 3 * ml;
   unsigned long long* own64 = reinterpret_cast<unsigned long long*>(a.stats) + (int64_t)f * ml;
-  int32_t* fin = a.stats + ((int64_t)a.n_frames + f) * 3 * ml;
   const bool packed = a.pack_sx != 0;
   auto add_own = [&](uint32_t L, int32_t x, int32_t y, int32_t n) {
     if (packed) {
@@ -209,6 +220,12 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
       atomicAdd(&own[3 * L + 1], y);
       atomicAdd(&own[3 * L + 2], n);
     }
+  };
+  // subtract size sz from label k's own size (the field holds at least sz:
+  // no borrow into the packed x field)
+  auto sub_own_size = [&](uint32_t k, int32_t sz) {
+    if (packed) atomicAdd(own64 + k, (unsigned long long)(-(long long)sz));
+    else atomicAdd(&own[3 * k + 2], -sz);
   };
   auto get_own = [&](int k, int32_t& x, int32_t& y, int32_t& n) {
     if (packed) {
@@ -251,10 +268,8 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
     }
     if (r + 1 < bh) load_row(r + 1, nx);
     // the neighbours' boundary columns (CLU:70-84 reads c-1 and c+1)
-    uint32_t l_prev = __shfl_up(prev_last, 1, 64), l_d = __shfl_up(d_last, 1, 64);
-    uint32_t r_prev = __shfl_down(prv[0], 1, 64);
-    if (lane == 0) l_prev = l_d = 0;
-    if (lane == 63) r_prev = 0;
+    const uint32_t l_prev = from_prev_lane(prev_last, 0u), l_d = from_prev_lane(d_last, 0u);
+    const uint32_t r_prev = from_next_lane(prv[0]);
     // up-row minima of the set metapixels; opening ones (no set causal neighbour)
     uint32_t nseed = 0;
     {
@@ -298,8 +313,7 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
       }
     }
     wave_incl_segmin(cb, cm);
-    uint32_t carry = __shfl_up(cm, 1, 64);  // exclusive: lanes before this one
-    if (lane == 0) carry = kInf;
+    const uint32_t carry = from_prev_lane(cm, kInf);  // exclusive: lanes before this one
     // labels; open the new labels (eq[L] = L)
     uint32_t seeds = 0, cur_last = 0;
     {
@@ -323,8 +337,7 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
       }
     }
     next += (int)total;
-    uint32_t l_cur = __shfl_up(cur_last, 1, 64);
-    if (lane == 0) l_cur = 0;
+    const uint32_t l_cur = from_prev_lane(cur_last, 0u);
     // statistics of the non-opening metapixels, one atomic per run of equal
     // labels; equivalence events flagged
     uint32_t events = 0;  // bit j: column c0 + j has a neighbour label != L
@@ -380,51 +393,66 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
   __threadfence();
   __syncthreads();
   const int n = next;
-  // postProcessing (CLU:115-127) without its order: fold own sums into fin
-  for (int k = lane; k < n; k += 64) {
-    if (k == 0) {
-      fin[0] = fin[1] = fin[2] = 0;
-      continue;
+  // postProcessing (CLU:115-127) in place, in ascending chunks of 64 labels:
+  // a label k with eq[k] != k adds its own (x, y, size) to eq[k] and keeps x
+  // and y with size 0.  CLU forwards what k holds when its turn comes, which
+  // is its own sums: every label that adds into k (eq[j] == k) is higher
+  // (eq[j] <= j), so it lies in k's chunk -- whose reads all precede its
+  // adds -- or in a later one.
+  for (int k0 = 0; k0 < n; k0 += 64) {
+    const int k = k0 + lane;
+    int32_t x = 0, y = 0, sz = 0;
+    int e = 0;
+    const bool live = k < n && k != 0;
+    if (live) {
+      e = eq[k];
+      get_own(k, x, y, sz);
     }
-    int32_t x, y, sz;
-    get_own(k, x, y, sz);
-    fin[3 * k] = x;
-    fin[3 * k + 1] = y;
-    fin[3 * k + 2] = eq[k] == k ? sz : 0;
+    if (live && e != k) {
+      add_own((uint32_t)e, x, y, sz);
+      sub_own_size((uint32_t)k, sz);
+    }
   }
+  // the adds performed (at L2) before the reads below; the L1 invalidated
   __threadfence();
   __syncthreads();
-  for (int k = lane + 0; k < n; k += 64) {
-    const int e = eq[k];
-    if (k != 0 && e != k) {
+  // the 8 largest (size desc, label asc): key = size << 32 | ~label (unique,
+  // never 0), eight passes over the labels, each a wave maximum below the
+  // last one.  When every size fits 16 bits the folded sizes are first copied
+  // into LDS over eq (dead after the fold), so the passes read LDS, not
+  // memory.
+  const bool lds_sizes = bw * bh < 65536;
+  if (lds_sizes) {
+#pragma unroll 4
+    for (int k = lane; k < n; k += 64) {
       int32_t x, y, sz;
       get_own(k, x, y, sz);
-      atomicAdd(&fin[3 * e], x);
-      atomicAdd(&fin[3 * e + 1], y);
-      atomicAdd(&fin[3 * e + 2], sz);
+      eq[k] = (uint16_t)sz;
     }
+    __syncthreads();
   }
-  __threadfence();
-  __syncthreads();
-  // the 8 largest (size desc, label asc): key = size << 32 | ~label
+  auto size_of = [&](int k) -> uint32_t {
+    if (lds_sizes) return eq[k];
+    int32_t x, y, sz;
+    get_own(k, x, y, sz);
+    return (uint32_t)sz;
+  };
   uint64_t last = ~0ull;
   int32_t* top = a.top + (int64_t)f * 24;
   TrikHsvTarget* tg = a.targets + (int64_t)f * 8;
   for (int i = 0; i < 8; ++i) {
     uint64_t best = 0;
+#pragma unroll 4
     for (int k = lane; k < n; k += 64) {
-      const uint64_t key = ((uint64_t)(uint32_t)fin[3 * k + 2] << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)k);
-      if (key < last && key > best) best = key;
+      const uint64_t key = ((uint64_t)size_of(k) << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)k);
+      best = key < last && key > best ? key : best;
     }
     best = wave_max_u64(best);
     last = best;
     if (lane == 0) {
       int32_t size = 0, sx = 0, sy = 0;
       if (best) {
-        const uint32_t k = 0xFFFFFFFFu - (uint32_t)best;
-        size = fin[3 * k + 2];
-        sx = fin[3 * k];
-        sy = fin[3 * k + 1];
+        get_own((int)(0xFFFFFFFFu - (uint32_t)best), sx, sy, size);
       }
       top[3 * i] = size;
       top[3 * i + 1] = sx;

@@ -292,7 +292,7 @@ struct BlobArgs {
   int32_t aligned4;          // frames, stride and line length 4-byte aligned
   uint8_t* meta;             // [n][H/4][W/4]: 1 for set metapixels
   uint16_t* labels;          // optional [n][H/4][W/4]: the clusterer's label map
-  int32_t* stats;            // scratch [2][n][max_labels][3]: own and folded {x, y, size}
+  int32_t* stats;            // scratch [n][max_labels][3] int32: the own {x, y, size}, folded in place
   int32_t max_labels;        // blob_max_labels(W/4, H/4)
   TrikHsvTarget* targets;    // [n][8]
   int32_t* top;              // [n][8][3]: size, sum_x, sum_y of the 8 largest clusters
