@@ -356,6 +356,28 @@ __device__ __forceinline__ void bin_add(uint32_t* cnt, uint32_t* lst, uint32_t v
   }
 }
 
+// The same for a wave whose active lanes are a prefix and hold consecutive
+// zone pixels (the zone walk): equal values of neighbouring lanes -- runs,
+// the common case on camera frames -- take one atomic by the run's first lane
+// (count = the run's length, last position = its last lane's).  A run head is
+// a lane whose left neighbour (DPP wave_shr:1) holds another value.
+template <bool kLast>
+__device__ __forceinline__ void bin_add_runs(uint32_t* cnt, uint32_t* lst, uint32_t v, uint32_t pos) {
+  const uint32_t lane = __lane_id();
+  const uint32_t left = (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFFu, (int)v, 0x138, 0xF, 0xF, false);
+  const bool head = lane == 0 || v != left;
+  const unsigned long long heads = __ballot(head);
+  const unsigned long long active = __ballot(true);  // a prefix of the wave
+  const unsigned long long above = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
+  const uint32_t end = above ? (uint32_t)__ffsll((long long)above) - 1u : (uint32_t)__popcll(active);
+  uint32_t p_last = 0;
+  if (kLast) p_last = (uint32_t)__shfl((int)pos, (int)(head ? end - 1u : lane), 64);
+  if (head) {
+    atomicAdd(&cnt[v], end - lane);
+    if (kLast) atomicMax(&lst[v], p_last);
+  }
+}
+
 // Per-wave sub-histograms (same-bin LDS atomics contend only within a wave).
 // kTwoPass = false: one pass records counts and last positions per value.
 // kTwoPass = true: pass 1 counts; pass 2 records the last position of the
@@ -409,7 +431,7 @@ __global__ __launch_bounds__(kBlock) void auto_range_kernel(AutoRangeArgs a) {
     hsv_bytes(fr, a, row, col, l43, l255, hv);
     const uint32_t pos = (uint32_t)((int64_t)row * a.width + col);  // scan order of s_rgb888hsv
 #pragma unroll
-    for (int k = 0; k < 3; ++k) bin_add<true, !kTwoPass>(cnt[wave][k], lst[kTwoPass ? 0 : wave][k], hv[k], pos);
+    for (int k = 0; k < 3; ++k) bin_add_runs<!kTwoPass>(cnt[wave][k], lst[kTwoPass ? 0 : wave][k], hv[k], pos);
   });
   __syncthreads();
   // merge the waves: counts add, last positions take the maximum
