@@ -186,10 +186,11 @@ __device__ __forceinline__ bool blob_target(int32_t size, int32_t sx, int32_t sy
 
 // Register form: lane l owns columns c0 = l*K .. c0+K-1 (K <= KMAX) and keeps
 // their set flags, up-row minima and the labels of rows r-1 / r in registers
-// (fully unrolled loops over KMAX with a j < K guard); the boundary values of
-// the neighbouring lanes come by one-lane shuffles.  LDS holds eq (and the
-// staged bitmap).
-template <int KMAX>
+// (fully unrolled loops over KMAX with a j < K guard; EXACT: K == KMAX, the
+// guards fold away -- VGA's 160 metapixel columns are K = 3); the boundary
+// values of the neighbouring lanes come by one-lane shifts.  LDS holds eq
+// (and the staged bitmap).
+template <int KMAX, bool EXACT>
 __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
   extern __shared__ uint16_t smem[];
   const int f = blockIdx.x, lane = threadIdx.x;
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
   };
   uint16_t* labels = a.labels ? a.labels + (int64_t)f * bw * bh : nullptr;
 
-  const int K = (bw + 63) / 64;
+  const int K = EXACT ? KMAX : (bw + 63) / 64;
   const int c0 = lane * K;
   uint32_t prv[KMAX], cur[KMAX], dd[KMAX], up[KMAX], nx[KMAX];
 #pragma unroll
@@ -543,8 +544,10 @@ int launch_blob(const BlobArgs& a, hipStream_t s) {
   b.meta_lds = TRIK_BLOB_META_LDS && a.n_frames < 2 * cus && lds + (size_t)bw * bh <= 40 * 1024 ? 1 : 0;
   if (b.meta_lds) lds += (size_t)bw * bh;
   const int K = (bw + 63) / 64;
-  auto kern = K <= 1 ? blob_ccl_kernel<1> : K <= 2 ? blob_ccl_kernel<2> : K <= 4 ? blob_ccl_kernel<4>
-            : K <= 8 ? blob_ccl_kernel<8> : K <= 16 ? blob_ccl_kernel<16> : blob_ccl_kernel<32>;
+  auto kern = K == 1 ? blob_ccl_kernel<1, true> : K == 2 ? blob_ccl_kernel<2, true>
+            : K == 3 ? blob_ccl_kernel<3, true> : K == 4 ? blob_ccl_kernel<4, true>
+            : K == 5 ? blob_ccl_kernel<5, true> : K <= 8 ? blob_ccl_kernel<8, false>
+            : K <= 16 ? blob_ccl_kernel<16, false> : blob_ccl_kernel<32, false>;
   hipLaunchKernelGGL(kern, dim3((unsigned)a.n_frames), dim3(64), lds, s, b);
   return hipGetLastError();
 }
