@@ -185,14 +185,20 @@ void preview_gather_kernel(PreviewArgs a, PreviewGeom g) {
 // The same preview when the scale maps are the 2:1 ones (output row r' is
 // written last by source row r0 + 2 r', output column c' by source column
 // 2 c' + 1 -- the reference's defaults, 640x480 -> 320x240) for packed YUYV:
-// output pixel c' is the odd pixel of source word c', so a lane reads 4
-// consecutive words (16 bytes, one load; a wave reads 1 KiB of one row) and
-// writes 4 output pixels (8 bytes).  No maps, no gather.  kQ units per lane,
-// 64 apart, loads issued together.
+// output pixel c' is the odd pixel of source word c', so a unit -- 4 output
+// pixels -- reads 4 consecutive words (16 bytes, one load; a wave reads 1 KiB
+// of one row) and writes 8 bytes.  No maps, no gather.  Lane t of the grid
+// takes units t, t + T, t + 2T, ... (T = the grid's lanes), kRowsQ of them per
+// round with their loads issued together; the (frame, row, group) of the next
+// unit follows from the current one by adding T's decomposition with carries
+// (one division per lane, not per unit).  The RGB565X value is packed from
+// the clamped channels directly; detection is range 0 (bit 0 of the hue and
+// sat&val masks).
 struct PreviewRowsGeom {
   FastDiv per_frame;  // out_h * groups per row
   FastDiv per_row;    // out_w / 4 groups per row
   uint32_t total;
+  uint32_t step_f, step_r, step_q;  // the grid's lane count T as (frames, rows, groups)
 };
 #ifndef TRIK_PREVIEW_ROWS_Q
 #define TRIK_PREVIEW_ROWS_Q 2
@@ -212,24 +218,35 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
   const int t = threadIdx.x;
   const uint32_t hue_lane = (uint32_t)offsetof(StripeTables, hue) + ((t % kHueCopies) << 2);
   const uint32_t m43_lane = (uint32_t)offsetof(StripeTables, m43) + ((t % kM43Copies) << 2);
-  const uint32_t gpr = g.per_row.d, lane = t & 63u, wave_step = (gridDim.x * blockDim.x) >> 6;
-  const uint32_t n_chunks = (g.total + 64u * kRowsQ - 1) / (64u * kRowsQ);
-  for (uint32_t ch = (blockIdx.x * blockDim.x + t) >> 6; ch < n_chunks; ch += wave_step) {
+  const uint32_t gpr = g.per_row.d, out_h = (uint32_t)a.out_h, nf = (uint32_t)a.n_frames;
+  // this lane's first unit
+  const uint32_t i0 = blockIdx.x * blockDim.x + (uint32_t)t;
+  uint32_t f = fdiv(i0, g.per_frame);
+  const uint32_t rem = i0 - f * g.per_frame.d;
+  uint32_t r = fdiv(rem, g.per_row);
+  uint32_t q = rem - r * gpr;
+  auto advance = [&]() {  // (f, r, q) += (step_f, step_r, step_q) with carries
+    q += g.step_q;
+    const bool cq = q >= gpr;
+    q = cq ? q - gpr : q;
+    r += g.step_r + (cq ? 1u : 0u);
+    const bool cr = r >= out_h;
+    r = cr ? r - out_h : r;
+    f += g.step_f + (cr ? 1u : 0u);
+  };
+  while (f < nf) {
     uint32_t ff[kRowsQ], rr[kRowsQ], qq[kRowsQ];
-    bool ok[kRowsQ];
     u32x4 w[kRowsQ];
 #pragma unroll
     for (int u = 0; u < kRowsQ; ++u) {
-      const uint32_t i0 = ch * 64u * kRowsQ + 64u * u + lane;
-      ok[u] = i0 < g.total;
-      const uint32_t i = ok[u] ? i0 : 0u;  // past the end: re-read unit 0, not stored
-      ff[u] = fdiv(i, g.per_frame);
-      const uint32_t rem = i - ff[u] * g.per_frame.d;
-      rr[u] = fdiv(rem, g.per_row);
-      qq[u] = rem - rr[u] * gpr;
-      const int64_t sr = (int64_t)a.rows2_first + 2 * (int64_t)rr[u];
+      ff[u] = f;
+      rr[u] = r;
+      qq[u] = q;
+      const uint32_t fl = f < nf ? f : 0u;  // past the end: re-read frame 0, not stored
       w[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
-          a.frames + (int64_t)ff[u] * a.frame_stride + sr * a.line_length + 16 * (int64_t)qq[u]));
+          a.frames + (int64_t)fl * a.frame_stride + (int64_t)((uint32_t)a.rows2_first + 2u * r) * a.line_length +
+          16 * (int64_t)q));
+      advance();
     }
 #pragma unroll
     for (int u = 0; u < kRowsQ; ++u) {
@@ -242,15 +259,17 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
         if (a.meta) {
           const int64_t sr = (int64_t)a.rows2_first + 2 * (int64_t)rr[u];
           const int64_t sc = 2 * (4 * (int64_t)qq[u] + k) + 1;
-          det = a.meta[((int64_t)ff[u] * (a.height >> 2) + (sr >> 2)) * (a.width >> 2) + (sc >> 2)];
+          det = a.meta[((int64_t)(ff[u] < nf ? ff[u] : 0u) * (a.height >> 2) + (sr >> 2)) * (a.width >> 2) +
+                       (sc >> 2)];
         } else {
           const uint32_t m = lds_u32(p.m43_addr), sv = lds_u8(p.sv_addr);
-          det = combine(lds_u32(phase2_addr(m, p, hue_lane)), sv) & 1u;
+          det = lds_u32(phase2_addr(m, p, hue_lane)) & sv & 1u;  // range 0 (combine keeps bit 0 in place)
         }
-        const uint32_t rgb = det ? 0x00ffffu : p.rgb888;
-        v[k] = ((rgb >> 19) & 0x001fu) | ((rgb >> 5) & 0x07e0u) | ((rgb << 8) & 0xf800u);
+        // RGB565X of det ? 0x00ffff : rgb888 (WSEQ:316-354): R >> 3 | (G >> 2) << 5 | (B >> 3) << 11
+        const uint32_t c565 = ((uint32_t)p.r >> 3) | (((uint32_t)p.g & 0xFCu) << 3) | (((uint32_t)p.b & 0xF8u) << 8);
+        v[k] = det ? 0xFFE0u : c565;
       }
-      if (ok[u]) {
+      if (ff[u] < nf) {
         uint2 o;
         o.x = v[0] | (v[1] << 16);
         o.y = v[2] | (v[3] << 16);
@@ -500,8 +519,14 @@ static int launch_rows2(const PreviewArgs& a, hipStream_t s) {
   g.per_row = make_div((uint32_t)gpr);
   g.total = (uint32_t)total;
   const int64_t blocks = (total + 1024LL * kRowsQ - 1) / (1024LL * kRowsQ), slots = 2LL * device_cus();
-  hipLaunchKernelGGL(preview_rows2_kernel, dim3((unsigned)(blocks < slots ? blocks : slots)), dim3(1024),
-                     a.meta ? 0 : sizeof(StripeTables), s, a, g);
+  const int64_t grid = blocks < slots ? blocks : slots;
+  {  // the grid's lane count as (frames, rows, groups): the kernel's per-unit step
+    const int64_t T = grid * 1024, pf = (int64_t)a.out_h * gpr;
+    g.step_f = (uint32_t)(T / pf);
+    g.step_r = (uint32_t)((T % pf) / gpr);
+    g.step_q = (uint32_t)(T % gpr);
+  }
+  hipLaunchKernelGGL(preview_rows2_kernel, dim3((unsigned)grid), dim3(1024), a.meta ? 0 : sizeof(StripeTables), s, a, g);
   return hipGetLastError();
 }
 

@@ -39,6 +39,7 @@ __device__ __forceinline__ uint32_t lds_u8(uint32_t addr) { return *(lds_u8_ptr)
 struct Phase1 {
   uint32_t m43_addr, sv_addr, diff, base;
   uint32_t rgb888;  // the clamped pixel (the preview's colour); dead code where unused
+  int r, g, b;      // its clamped channels (the 2:1 preview packs RGB565X from them)
 };
 constexpr int log2i(int v) { return v <= 1 ? 0 : 1 + log2i(v / 2); }
 constexpr int kM43Shift = log2i(4 * kM43Copies);  // byte stride of one m43 entry's copies
@@ -59,6 +60,9 @@ __device__ __forceinline__ Phase1 phase1(uint32_t w, uint32_t wc, uint32_t m43_l
   const int mn = min(r, min(g, b));
   Phase1 p;
   p.rgb888 = ((uint32_t)r << 16) | ((uint32_t)g << 8) | (uint32_t)b;
+  p.r = r;
+  p.g = g;
+  p.b = b;
   p.m43_addr = ((uint32_t)(mx - mn) << kM43Shift) + m43_lane;
   p.sv_addr = __umul24((uint32_t)mx, (uint32_t)kSvStride) + (uint32_t)mn;
   const bool eqG = mx == g, eqB = mx == b;
