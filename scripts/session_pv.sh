@@ -1,6 +1,6 @@
 #!/bin/bash
 set -u
 cd "$GRAFT_REPO_ROOT"; OUT=gpurun_out/pv; mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests/test_gpu_operator.py tests/test_gpu_object_sensor.py tests/test_gpu_blob.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_operator.py tests/test_gpu_object_sensor.py tests/test_gpu_blob.py tests/test_gpu_line.py tests/test_gpu_wline.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1
 rc=$?; tail -3 $OUT/tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python scripts/bench_operator.py --no-cpu > $OUT/operator.json 2>&1; rc=$?; tail -c 1500 $OUT/operator.json; exit $rc

@@ -337,6 +337,7 @@ struct TrikCvHandle {
   size_t d_maps_cap = 0;
   int maps_key[6] = {-1, -1, -1, -1, -1, -1};
   int32_t maps_rows2 = -1;  // first source row when the maps are the 2:1 ones, else -1
+  int32_t maps_rows2_c0 = 0, maps_rows2_c1 = 0;  // the output columns the 2:1 maps write
   std::vector<uint32_t> h_maps;
   StreamUses maps_users;
 
@@ -855,8 +856,15 @@ int32_t ensure_maps(TrikCvHandle* h, int w, int hgt, int ow, int oh, hipStream_t
   const uint32_t* last_col = last_row + oh;
   bool rows2 = oh > 0 && ow > 0 && (int32_t)last_row[0] >= 0;
   for (int r = 0; rows2 && r < oh; ++r) rows2 = (int32_t)last_row[r] == (int32_t)last_row[0] + 2 * r;
-  for (int c = 0; rows2 && c < ow; ++c) rows2 = (int32_t)last_col[c] == 2 * c + 1;
+  // the written columns: one window [c0, c1) with last_col[c] = 2c + 1, -1 outside
+  int c0 = 0, c1 = ow;
+  while (c0 < ow && (int32_t)last_col[c0] < 0) ++c0;
+  while (c1 > c0 && (int32_t)last_col[c1 - 1] < 0) --c1;
+  for (int c = 0; rows2 && c < ow; ++c)
+    rows2 = (c >= c0 && c < c1) ? (int32_t)last_col[c] == 2 * c + 1 : (int32_t)last_col[c] < 0;
   h->maps_rows2 = rows2 ? (int32_t)last_row[0] : -1;
+  h->maps_rows2_c0 = c0;
+  h->maps_rows2_c1 = c1;
   return 0;
 }
 
@@ -881,6 +889,8 @@ PreviewArgs preview_args(const TrikCvHandle* h, const TrikHsvFrameBatch& b,
   a.last_row = reinterpret_cast<const int32_t*>(a.hi2ho + b.height);
   a.last_col = a.last_row + oh;
   a.rows2_first = h->maps_rows2;
+  a.rows2_c0 = h->maps_rows2_c0;
+  a.rows2_c1 = h->maps_rows2_c1;
   return a;
 }
 
@@ -891,6 +901,7 @@ int32_t preview_tables(TrikCvHandle* h, PreviewArgs& pa, const TRIK_VIDTRANSCODE
   if (rc) return rc;
   pa.range = pack_range(range);
   pa.tables = (*set)->d_stripe;
+  pa.hue_free = !(*set)->detect.empty() && (*set)->detect[0] != kDetectFull ? 1 : 0;
   return 0;
 }
 

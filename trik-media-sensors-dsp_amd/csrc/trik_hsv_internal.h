@@ -202,9 +202,13 @@ struct PreviewArgs {
   // ov7670 multi-blob preview: when set, a pixel is "detected" iff its 4x4
   // metapixel is set ([n][H/4][W/4], OSEQ:411-413) instead of by `range`
   const uint8_t* meta = nullptr;
-  // >= 0 when the maps are the 2:1 ones: last_row[r] = rows2_first + 2 r and
-  // last_col[c] = 2 c + 1 for every output row and column (preview_rows2_kernel)
-  int32_t rows2_first = -1;
+  // >= 0 when the maps are the 2:1 ones: last_row[r] = rows2_first + 2 r for
+  // every output row and last_col[c] = 2 c + 1 for the output columns in
+  // [rows2_c0, rows2_c1), -1 (not written) outside (preview_rows2_kernel)
+  int32_t rows2_first = -1, rows2_c0 = 0, rows2_c1 = 0;
+  // range 0 accepts every hue (its detect_mode() is not kDetectFull): the 2:1
+  // kernel tests the sat&val mask alone
+  int32_t hue_free = 0;
 };
 
 // Auto HSV range of N frames (trik_hsv_operator.hip); out[f][6] = detectHue,

@@ -184,19 +184,24 @@ void preview_gather_kernel(PreviewArgs a, PreviewGeom g) {
 
 // The same preview when the scale maps are the 2:1 ones (output row r' is
 // written last by source row r0 + 2 r', output column c' by source column
-// 2 c' + 1 -- the reference's defaults, 640x480 -> 320x240) for packed YUYV:
-// output pixel c' is the odd pixel of source word c', so a unit -- 4 output
-// pixels -- reads 4 consecutive words (16 bytes, one load; a wave reads 1 KiB
-// of one row) and writes 8 bytes.  No maps, no gather.  Lane t of the grid
-// takes units t, t + T, t + 2T, ... (T = the grid's lanes), kRowsQ of them per
-// round with their loads issued together; the (frame, row, group) of the next
-// unit follows from the current one by adding T's decomposition with carries
-// (one division per lane, not per unit).  The RGB565X value is packed from
-// the clamped channels directly; detection is range 0 (bit 0 of the hue and
-// sat&val masks).
+// 2 c' + 1 -- the reference's defaults, 640x480 -> 320x240), with the written
+// output columns one contiguous window [rows2_c0, rows2_c1) (the line
+// sensor's 5 <= col <= W - 5; zero outside).  Output pixel c' is the odd
+// pixel of source pixel pair c'.  A unit reads 16 bytes per plane and writes
+// its output pixels as 8-byte stores: packed YUYV, 4 words -> 4 pixels (a
+// wave reads 1 KiB of one row); ov7670, 16 luma + 16 chroma bytes -> 8 pixels
+// (U = odd chroma byte, OSEQ:369-373).  No maps, no gather.  Lane t of the
+// grid takes units t, t + T, t + 2T, ... (T = the grid's lanes), kRowsQ of
+// them per round with their loads issued together; the (frame, row, group) of
+// the next unit follows from the current one by adding T's decomposition with
+// carries (one division per lane, not per unit).  The RGB565X value is packed
+// from the clamped channels directly; detection is range 0 (bit 0 of the hue
+// and sat&val masks; HUEFREE, a range that accepts every hue -- the line
+// sensors' V ranges: the sat&val mask alone) or the metapixel flag
+// (multi-blob).  WIN: some output columns are outside the written window.
 struct PreviewRowsGeom {
   FastDiv per_frame;  // out_h * groups per row
-  FastDiv per_row;    // out_w / 4 groups per row
+  FastDiv per_row;    // groups per row (out_w / pixels per unit)
   uint32_t total;
   uint32_t step_f, step_r, step_q;  // the grid's lane count T as (frames, rows, groups)
 };
@@ -204,10 +209,13 @@ struct PreviewRowsGeom {
 #define TRIK_PREVIEW_ROWS_Q 2
 #endif
 constexpr int kRowsQ = TRIK_PREVIEW_ROWS_Q;
+template <int LAYOUT, bool WIN, bool HUEFREE>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8)))
 void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
   using namespace stripe_px;
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  constexpr bool YUYV = LAYOUT == TRIK_HSV_LAYOUT_YUYV;
+  constexpr int PX = YUYV ? 4 : 8;  // output pixels per unit
   if (!a.meta) {
     const u32x4* src = reinterpret_cast<const u32x4*>(a.tables);
     typedef __attribute__((address_space(3))) u32x4* lds_u128_wptr;
@@ -219,6 +227,7 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
   const uint32_t hue_lane = (uint32_t)offsetof(StripeTables, hue) + ((t % kHueCopies) << 2);
   const uint32_t m43_lane = (uint32_t)offsetof(StripeTables, m43) + ((t % kM43Copies) << 2);
   const uint32_t gpr = g.per_row.d, out_h = (uint32_t)a.out_h, nf = (uint32_t)a.n_frames;
+  const int64_t plane = (int64_t)a.height * a.line_length;
   // this lane's first unit
   const uint32_t i0 = blockIdx.x * blockDim.x + (uint32_t)t;
   uint32_t f = fdiv(i0, g.per_frame);
@@ -236,31 +245,45 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
   };
   while (f < nf) {
     uint32_t ff[kRowsQ], rr[kRowsQ], qq[kRowsQ];
-    u32x4 w[kRowsQ];
+    u32x4 w[kRowsQ], wc[kRowsQ];
 #pragma unroll
     for (int u = 0; u < kRowsQ; ++u) {
       ff[u] = f;
       rr[u] = r;
       qq[u] = q;
       const uint32_t fl = f < nf ? f : 0u;  // past the end: re-read frame 0, not stored
-      w[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
-          a.frames + (int64_t)fl * a.frame_stride + (int64_t)((uint32_t)a.rows2_first + 2u * r) * a.line_length +
-          16 * (int64_t)q));
+      const uint8_t* src = a.frames + (int64_t)fl * a.frame_stride +
+                           (int64_t)((uint32_t)a.rows2_first + 2u * r) * a.line_length + 16 * (int64_t)q;
+      w[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
+      if (!YUYV) wc[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + plane));
       advance();
     }
 #pragma unroll
     for (int u = 0; u < kRowsQ; ++u) {
-      const uint32_t ws[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
-      uint32_t v[4];
+      uint32_t ws[PX];
+      if (YUYV) {
+        ws[0] = w[u].x; ws[1] = w[u].y; ws[2] = w[u].z; ws[3] = w[u].w;
+      } else {  // the word (-, U, Y1, V) of output pixel 2d + j: luma byte 2j + 1, chroma bytes 2j, 2j + 1
+        const uint32_t yy[4] = {w[u].x, w[u].y, w[u].z, w[u].w}, cc[4] = {wc[u].x, wc[u].y, wc[u].z, wc[u].w};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const Phase1 p = phase1<1>(ws[k], ws[k] ^ 0xFF00FF00u, m43_lane);  // the odd pixel, Y1
+        for (int d = 0; d < 4; ++d) {
+          ws[(2 * d) % PX] = __builtin_amdgcn_perm(cc[d], yy[d], 0x0401050Cu);
+          ws[(2 * d + 1) % PX] = __builtin_amdgcn_perm(cc[d], yy[d], 0x0603070Cu);
+        }
+      }
+      uint32_t v[PX];
+#pragma unroll
+      for (int k = 0; k < PX; ++k) {
+        const Phase1 p = phase1<1>(ws[k], ws[k] ^ 0xFF00FF00u, m43_lane);  // the odd pixel: Y in byte 2
+        const uint32_t c = PX * qq[u] + (uint32_t)k;                        // its output column
         uint32_t det;
         if (a.meta) {
           const int64_t sr = (int64_t)a.rows2_first + 2 * (int64_t)rr[u];
-          const int64_t sc = 2 * (4 * (int64_t)qq[u] + k) + 1;
+          const int64_t sc = 2 * (int64_t)c + 1;
           det = a.meta[((int64_t)(ff[u] < nf ? ff[u] : 0u) * (a.height >> 2) + (sr >> 2)) * (a.width >> 2) +
                        (sc >> 2)];
+        } else if (HUEFREE) {
+          det = lds_u8(p.sv_addr) & 1u;
         } else {
           const uint32_t m = lds_u32(p.m43_addr), sv = lds_u8(p.sv_addr);
           det = lds_u32(phase2_addr(m, p, hue_lane)) & sv & 1u;  // range 0 (combine keeps bit 0 in place)
@@ -268,13 +291,17 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
         // RGB565X of det ? 0x00ffff : rgb888 (WSEQ:316-354): R >> 3 | (G >> 2) << 5 | (B >> 3) << 11
         const uint32_t c565 = ((uint32_t)p.r >> 3) | (((uint32_t)p.g & 0xFCu) << 3) | (((uint32_t)p.b & 0xF8u) << 8);
         v[k] = det ? 0xFFE0u : c565;
+        if (WIN) v[k] = c >= (uint32_t)a.rows2_c0 && c < (uint32_t)a.rows2_c1 ? v[k] : 0u;
       }
       if (ff[u] < nf) {
-        uint2 o;
-        o.x = v[0] | (v[1] << 16);
-        o.y = v[2] | (v[3] << 16);
-        *reinterpret_cast<uint2*>(a.previews + (int64_t)ff[u] * a.preview_stride + (int64_t)rr[u] * a.out_ll +
-                                  8 * (int64_t)qq[u]) = o;
+        uint8_t* dst = a.previews + (int64_t)ff[u] * a.preview_stride + (int64_t)rr[u] * a.out_ll + 2 * PX * (int64_t)qq[u];
+#pragma unroll
+        for (int h = 0; h < PX / 4; ++h) {
+          uint2 o;
+          o.x = v[4 * h] | (v[4 * h + 1] << 16);
+          o.y = v[4 * h + 2] | (v[4 * h + 3] << 16);
+          *reinterpret_cast<uint2*>(dst + 8 * h) = o;
+        }
       }
     }
   }
@@ -501,7 +528,9 @@ __global__ __launch_bounds__(kBlock) void auto_range_kernel(AutoRangeArgs a) {
 // The 2:1 row kernel when the maps, layout and alignment allow (see
 // preview_rows2_kernel); hipErrorNotSupported otherwise.
 static int launch_rows2(const PreviewArgs& a, hipStream_t s) {
-  if (a.rows2_first < 0 || a.layout != TRIK_HSV_LAYOUT_YUYV || a.out_w % 4 || a.out_ll != 2 * a.out_w ||
+  const bool yuyv = a.layout == TRIK_HSV_LAYOUT_YUYV;
+  const int px = yuyv ? 4 : 8;
+  if (a.rows2_first < 0 || (!yuyv && a.layout != TRIK_HSV_LAYOUT_OV7670) || a.out_w % px || a.out_ll != 2 * a.out_w ||
       (!a.meta && !a.tables))
     return hipErrorNotSupported;
   const auto al = [](int64_t v, int64_t m) { return v % m == 0; };
@@ -509,10 +538,20 @@ static int launch_rows2(const PreviewArgs& a, hipStream_t s) {
       (a.n_frames > 1 && !al(a.frame_stride, 16)) || !al((int64_t)reinterpret_cast<uintptr_t>(a.previews), 8) ||
       (a.n_frames > 1 && !al(a.preview_stride, 8)))
     return hipErrorNotSupported;
-  const int64_t gpr = a.out_w / 4, total = (int64_t)a.n_frames * a.out_h * gpr;
+  const int64_t gpr = a.out_w / px, total = (int64_t)a.n_frames * a.out_h * gpr;
   if (total >= (1ll << 31)) return hipErrorNotSupported;
   if (total == 0) return hipSuccess;
-  hipError_t e = set_dynamic_lds(reinterpret_cast<const void*>(preview_rows2_kernel), 80 * 1024);
+  const bool win = a.rows2_c0 > 0 || a.rows2_c1 < a.out_w, hue_free = a.hue_free && !a.meta;
+  using Kern = void (*)(PreviewArgs, PreviewRowsGeom);
+  static const Kern kerns[2][2][2] = {
+      {{preview_rows2_kernel<TRIK_HSV_LAYOUT_YUYV, false, false>, preview_rows2_kernel<TRIK_HSV_LAYOUT_YUYV, false, true>},
+       {preview_rows2_kernel<TRIK_HSV_LAYOUT_YUYV, true, false>, preview_rows2_kernel<TRIK_HSV_LAYOUT_YUYV, true, true>}},
+      {{preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, false, false>,
+        preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, false, true>},
+       {preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, true, false>,
+        preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, true, true>}}};
+  const Kern kern = kerns[yuyv ? 0 : 1][win ? 1 : 0][hue_free ? 1 : 0];
+  hipError_t e = set_dynamic_lds(reinterpret_cast<const void*>(kern), 80 * 1024);
   if (e != hipSuccess) return e;
   PreviewRowsGeom g;
   g.per_frame = make_div((uint32_t)(a.out_h * gpr));
@@ -526,7 +565,8 @@ static int launch_rows2(const PreviewArgs& a, hipStream_t s) {
     g.step_r = (uint32_t)((T % pf) / gpr);
     g.step_q = (uint32_t)(T % gpr);
   }
-  hipLaunchKernelGGL(preview_rows2_kernel, dim3((unsigned)grid), dim3(1024), a.meta ? 0 : sizeof(StripeTables), s, a, g);
+  const size_t lds = a.meta ? 0 : sizeof(StripeTables);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(1024), lds, s, a, g);
   return hipGetLastError();
 }
 
