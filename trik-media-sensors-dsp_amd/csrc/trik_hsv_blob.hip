@@ -114,9 +114,6 @@ void blob_meta_kernel(BlobArgs a, MetaGeom g) {
   }
 }
 
-#ifndef TRIK_BLOB_META_LDS
-#define TRIK_BLOB_META_LDS 1  // 0: never stage the bitmap (A/B runs)
-#endif
 constexpr uint32_t kInf = 0xFFFFu;
 
 // Inclusive wave scans with DPP (row_shr 1/2/4/8 inside 16-lane rows, then
@@ -541,7 +538,7 @@ int launch_blob(const BlobArgs& a, hipStream_t s) {
   // (latency); large batches read it from L2 instead, so that the eq table
   // alone bounds the residency (VGA: 16 frames per CU instead of 5; 4096
   // frames 1.59 -> 1.30 ms with the chroma-run bitmap kernel)
-  b.meta_lds = TRIK_BLOB_META_LDS && a.n_frames < 2 * cus && lds + (size_t)bw * bh <= 40 * 1024 ? 1 : 0;
+  b.meta_lds = a.n_frames < 2 * cus && lds + (size_t)bw * bh <= 40 * 1024 ? 1 : 0;
   if (b.meta_lds) lds += (size_t)bw * bh;
   const int K = (bw + 63) / 64;
   auto kern = K == 1 ? blob_ccl_kernel<1, true> : K == 2 ? blob_ccl_kernel<2, true>

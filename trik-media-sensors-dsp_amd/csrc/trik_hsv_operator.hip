@@ -51,15 +51,7 @@ __constant__ Luts c_luts = make_luts();
 // per-pixel arithmetic (phase1 also yields the clamped colour); with
 // a.meta set (the multi-blob preview) detection is the metapixel flag and no
 // tables are staged.  Every byte of the out_h x out_ll preview is written.
-#ifndef TRIK_PREVIEW_MAP_LDS
-#define TRIK_PREVIEW_MAP_LDS 1
-#endif
-#ifndef TRIK_PREVIEW_ROWS2
-#define TRIK_PREVIEW_ROWS2 1  // the 2:1 row kernel where it applies
-#endif
-#ifndef TRIK_PREVIEW_Q
-#define TRIK_PREVIEW_Q 2
-#endif
+constexpr int kPreviewQ = 2;  // output groups per lane of the gather
 struct PreviewGeom {
   FastDiv per_frame;  // out_h * quads per row
   FastDiv per_row;    // quads per row
@@ -97,7 +89,7 @@ void preview_gather_kernel(PreviewArgs a, PreviewGeom g) {
   // a wave stays on consecutive groups), in phases (positions, map loads, frame
   // loads, arithmetic, stores) so that a thread's loads are in flight together:
   // the loop is bound by the map -> frame -> LDS chain, not by bytes
-  constexpr int kQ = TRIK_PREVIEW_Q;
+  constexpr int kQ = kPreviewQ;
   const uint32_t lane = t & 63u, wave_step = (gridDim.x * blockDim.x) >> 6;
   const uint32_t n_chunks = (g.total + 64u * kQ - 1) / (64u * kQ);
   for (uint32_t ch = (blockIdx.x * blockDim.x + t) >> 6; ch < n_chunks; ch += wave_step) {
@@ -205,10 +197,7 @@ struct PreviewRowsGeom {
   uint32_t total;
   uint32_t step_f, step_r, step_q;  // the grid's lane count T as (frames, rows, groups)
 };
-#ifndef TRIK_PREVIEW_ROWS_Q
-#define TRIK_PREVIEW_ROWS_Q 2
-#endif
-constexpr int kRowsQ = TRIK_PREVIEW_ROWS_Q;
+constexpr int kRowsQ = 2;  // units per lane and round
 template <int LAYOUT, bool WIN, bool HUEFREE>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8)))
 void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
@@ -348,9 +337,7 @@ __global__ __launch_bounds__(64) void overlay_kernel(PreviewArgs a, const TrikHs
 }
 
 constexpr int kRangeBlock = 256;
-#ifndef TRIK_RANGE_WIDE_FRAMES
-#define TRIK_RANGE_WIDE_FRAMES 32
-#endif
+constexpr int kRangeWideFrames = 32;  // batches up to this size: 1024 lanes per frame
 
 // H, S, V bytes of one pixel (WSEQ:207-249), branch-free as the hot kernel's
 // phase1 (clamp8_shift6 on v_dot4 presums, the hue case as selects), with
@@ -571,7 +558,7 @@ static int launch_rows2(const PreviewArgs& a, hipStream_t s) {
 }
 
 static int launch_gather(const PreviewArgs& a, hipStream_t s) {
-  if (TRIK_PREVIEW_ROWS2) {
+  {  // the 2:1 row kernel where it applies
     const int e = launch_rows2(a, s);
     if (e != hipErrorNotSupported) return e;
   }
@@ -591,12 +578,12 @@ static int launch_gather(const PreviewArgs& a, hipStream_t s) {
   // every source coordinate fits u16
   const uint32_t tables_bytes = a.meta ? 16u : (uint32_t)sizeof(StripeTables);
   const int64_t map_bytes = 2LL * (a.out_w + a.out_h);
-  g.map_off = TRIK_PREVIEW_MAP_LDS && a.width < 65535 && a.height < 65535 &&
+  g.map_off = a.width < 65535 && a.height < 65535 &&
                       tables_bytes + map_bytes <= 80 * 1024
                   ? tables_bytes
                   : 0u;
   const size_t lds = g.map_off ? (size_t)(tables_bytes + map_bytes) : (a.meta ? 0 : sizeof(StripeTables));
-  const int64_t blocks = (total + 1024LL * TRIK_PREVIEW_Q - 1) / (1024LL * TRIK_PREVIEW_Q), slots = 2LL * cus;
+  const int64_t blocks = (total + 1024LL * kPreviewQ - 1) / (1024LL * kPreviewQ), slots = 2LL * cus;
   hipLaunchKernelGGL(preview_gather_kernel, dim3((unsigned)(blocks < slots ? blocks : slots)), dim3(1024),
                      lds, s, a, g);
   return hipGetLastError();
@@ -622,7 +609,7 @@ int launch_auto_range(const AutoRangeArgs& a, hipStream_t s) {
   // the zone is a latency-bound chain per lane, 4x shorter
   if (a.n_frames >= 512)
     hipLaunchKernelGGL((auto_range_kernel<true, kRangeBlock>), dim3((unsigned)a.n_frames), dim3(kRangeBlock), 0, s, a);
-  else if (a.n_frames <= TRIK_RANGE_WIDE_FRAMES)
+  else if (a.n_frames <= kRangeWideFrames)
     hipLaunchKernelGGL((auto_range_kernel<false, 1024>), dim3((unsigned)a.n_frames), dim3(1024), 0, s, a);
   else
     hipLaunchKernelGGL((auto_range_kernel<false, kRangeBlock>), dim3((unsigned)a.n_frames), dim3(kRangeBlock), 0, s, a);
