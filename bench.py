@@ -139,9 +139,29 @@ def cpu_baseline(args, width, height, ll, n_ranges, host, gpu_sums):
             "value_share": round(n * px / dt / 1e6, 3), "share_threads": share,
             "share_sample": f"{n} frames, {share} threads (the box's CPU share per GPU), {dt:.2f} s",
             "value_1core": round(n1 * px / dt1 / 1e6, 3),
-            "machine_threads": machine, "threads_allowed": allowed,
+            "machine_threads": machine, "threads_allowed": allowed, "cgroup_cpu_quota": cgroup_cpus(),
             "value_intrinsic_emulation": round(ne * px / dt2 / 1e6, 3),
             "cpu_model": cpu_model()}, parity
+
+
+def cgroup_cpus():
+    """The CPU bandwidth quota of this process's cgroup in CPUs (cgroup v2
+    cpu.max or v1 cfs quota/period), or None when unlimited/unknown: a box
+    that shows 256 hardware threads may grant a GPU job far fewer."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else round(q / per, 2)
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_model():
