@@ -558,6 +558,12 @@ struct ChromaGeom {
   int32_t steps_last;  // steps of a frame's last tile
   int64_t n_tiles;
   int32_t flush_rounds;  // drain rounds between unpacks of the 16-bit exception sums
+  // divisions of the per-unit setup by multiplication: units per tile (the
+  // workgroup's waves) and tiles per frame (wave-uniform: SALU), and a lane's
+  // index in its tile by cpr: ro = lt * cpr_inv >> 20 with cpr_inv =
+  // ceil(2^20 / cpr), exact for lt < 1024 and cpr < 1024
+  FastDiv fd_units, fd_tiles;
+  uint32_t cpr_inv;
 };
 
 // The 12 per-lane values (3 per range, 4 ranges) summed over the wave: two
@@ -683,17 +689,18 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     uint32_t next = 0;
     if (lane == 0) next = __hip_atomic_fetch_add((__attribute__((address_space(3))) uint32_t*)(uintptr_t)kLdsUnits,
                                                  1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    // (the divisions run on the VALU: their wave-uniform results are moved to
+    // (wave-uniform divisions by multiplication; the results are moved to
     // SGPRs, else everything derived from them stays in VGPRs)
     // (tile indices fit 32 bits: chroma_geometry)
-    const uint32_t tl = __builtin_amdgcn_readfirstlane(u / U);
+    const uint32_t tl = __builtin_amdgcn_readfirstlane(fdiv(u, g.fd_units));
     const uint32_t tile = (uint32_t)t_begin + tl;
-    const int f = (int)__builtin_amdgcn_readfirstlane(tile / (uint32_t)g.tiles_per_frame);
+    const int f = (int)__builtin_amdgcn_readfirstlane(fdiv(tile, g.fd_tiles));
     const int trem = (int)(tile - (uint32_t)f * (uint32_t)g.tiles_per_frame);
-    const int lt = (int)((u - tl * U) * 64u) + lane;  // the lane's index in the tile
+    const int lt = (int)((u - tl * U) * 64u) + lane;  // the lane's index in the tile (< 1024)
     const bool active = lt < g.k * g.cpr;
-    const int col = active ? lt % g.cpr : 0;
-    const int ro = active ? lt / g.cpr : 0;
+    const uint32_t q = __umul24((uint32_t)lt, g.cpr_inv) >> 20;  // lt / cpr
+    const int col = active ? lt - (int)__umul24(q, (uint32_t)g.cpr) : 0;
+    const int ro = active ? (int)q : 0;
     const int col_bytes = LAYOUT == TRIK_HSV_LAYOUT_YUYV ? col * 16 : col * 2 * CW;
     const uint32_t x0 = (uint32_t)col * (SPLIT ? 8u : 2u * CW);
     const uint32_t voff = (uint32_t)ro * (uint32_t)a.line_length + (uint32_t)col_bytes;
@@ -722,7 +729,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         const uint32_t n = (ex.EN >> (8 * rr)) & 0xFFu;
         v[3 * rr + 0] += n;
         v[3 * rr + 1] += (sx >> sh) & 0xFFFFu;
-        v[3 * rr + 2] += ((sy >> sh) & 0xFFFFu) + (uint32_t)r0 * n;
+        v[3 * rr + 2] += ((sy >> sh) & 0xFFFFu) + __umul24((uint32_t)r0, n);  // (24-bit: full-rate multiply)
       }
       ex.EN = ex.SX02 = ex.SX13 = ex.SY02 = ex.SY13 = 0;
       ex.rounds = 0;
@@ -955,24 +962,43 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     Qb += Bb;
 
     uint32_t acc[12] = {};
+    // x offsets within the chunk: 2 (i & 3) (+ dx for the second piece) or
+    // 2 i; nb2: pixels of the second pieces (rows + half, columns + dx).  The
+    // weighted sums are formed on the byte-packed counters with ranges 0, 2
+    // (A) and 1, 3 (B) spread into 16-bit halves (one v_perm each), two
+    // ranges per operation: halves stay below 2^16 (P bytes <= 2 * kMaxSteps,
+    // O bytes <= 8 * kMaxSteps).
+    auto half_a = [](uint32_t v) { return __builtin_amdgcn_perm(0u, v, 0x0C020C00u); };  // bytes 0, 2
+    auto half_b = [](uint32_t v) { return __builtin_amdgcn_perm(0u, v, 0x0C030C01u); };  // bytes 1, 3
+    uint32_t XA = half_a(O), XB = half_b(O), NA = 0, NB = 0;
+    if (SPLIT) {
+      const uint32_t S1 = P[1] + P[5], S2 = P[2] + P[6], S3 = P[3] + P[7];  // bytes <= 4 * kMaxSteps
+      XA += 2u * half_a(S1) + 4u * half_a(S2) + 6u * half_a(S3);
+      XB += 2u * half_b(S1) + 4u * half_b(S2) + 6u * half_b(S3);
+      const uint32_t N = P[4] + P[5] + P[6] + P[7];  // bytes <= 8 * kMaxSteps
+      NA = half_a(N);
+      NB = half_b(N);
+    } else {
+#pragma unroll
+      for (int i = 1; i < CW; ++i) {
+        XA += (uint32_t)(2 * i) * half_a(P[i]);
+        XB += (uint32_t)(2 * i) * half_b(P[i]);
+      }
+    }
+    static_assert(8 * kMaxSteps + 2 * kChunkWords * kChunkWords * 2 * kMaxSteps < 65536, "16-bit halves");
 #pragma unroll
     for (int rr = 0; rr < NR; ++rr) {
-      const int sh = 8 * rr;
-      const uint32_t c = ((rr & 1) ? (CumB >> ((rr >> 1) * 16)) : (CumA >> ((rr >> 1) * 16))) & 0xFFFFu;
-      // x offsets within the chunk: 2 (i & 3) (+ dx for the second piece) or 2 i;
-      // nb2: pixels of the second pieces (rows + half, columns + dx)
-      uint32_t wx = (O >> sh) & 0xFFu, nb2 = 0;
-#pragma unroll
-      for (int i = 1; i < CW; ++i) wx += (uint32_t)(SPLIT ? 2 * (i & 3) : 2 * i) * ((P[i] >> sh) & 0xFFu);
+      const int hs = (rr >> 1) * 16;
+      const uint32_t c = ((rr & 1) ? (CumB >> hs) : (CumA >> hs)) & 0xFFFFu;
+      uint32_t wx = (((rr & 1) ? XB : XA) >> hs) & 0xFFFFu, nb2 = 0;
       if (SPLIT) {
-#pragma unroll
-        for (int i = 4; i < CW; ++i) nb2 += (P[i] >> sh) & 0xFFu;
+        nb2 = (((rr & 1) ? NB : NA) >> hs) & 0xFFFFu;
         wx += __umul24(dx, nb2);
       }
       const uint32_t qq = ((rr & 1) ? (Qb >> ((rr >> 1) * 16)) : (Qa >> ((rr >> 1) * 16))) & 0xFFFFu;
       acc[3 * rr + 0] = c;
       acc[3 * rr + 1] = __umul24(x0, c) + wx;
-      acc[3 * rr + 2] = __umul24((uint32_t)y0, c) + (uint32_t)g.rstep * ((uint32_t)steps * c - qq) +
+      acc[3 * rr + 2] = __umul24((uint32_t)y0, c) + __umul24((uint32_t)g.rstep, __umul24((uint32_t)steps, c) - qq) +
                         __umul24((uint32_t)half, nb2);
     }
     unpack_exc(acc);
@@ -1247,6 +1273,9 @@ bool chroma_geometry(const KernelArgs& a, ChromaGeom& g) {
   if (2LL * span > 65535) return false;
   int r = 65535 / (2 * span);
   g.flush_rounds = r > 127 ? 127 : r;
+  g.fd_units = make_div((uint32_t)((g.k * g.cpr + 63) / 64));  // the launch's waves per workgroup
+  g.fd_tiles = make_div((uint32_t)g.tiles_per_frame);
+  g.cpr_inv = (uint32_t)(((1u << 20) + (uint32_t)cpr - 1) / (uint32_t)cpr);
   return true;
 }
 
