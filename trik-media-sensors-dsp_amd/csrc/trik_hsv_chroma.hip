@@ -56,7 +56,12 @@ constexpr int kQueueCap = 128;  // blob kernel, entries per wave: < 64 waiting +
 // compactions, not one per word slot.  kRecCap records per wave is what the
 // LDS image leaves; a step starts with < 64 records queued.
 constexpr int kHotLanes = 960;
-constexpr int kRecCap = 73;
+// the hot kernel's workgroup: 16 waves (4 per SIMD) whatever the tile's
+// lane count (<= kHotLanes: 15 wave-sized units at VGA); the waves pull the
+// units, so one more wave than units per tile costs nothing and fills the
+// fourth SIMD
+constexpr int kHotWaves = 16;
+constexpr int kRecCap = 70;
 
 // LDS image of the chroma kernel (dynamic LDS from address 0).  The block
 // masks and the mask-pair table sit below 64 KiB so their reads take an
@@ -75,9 +80,9 @@ static_assert(kLdsBlocks + 8192 <= kLdsPairs, "LDS layout");
 // words (kRecCap x 4 B per wave): f (bits 0-3: the piece's flagged words) |
 // x / 8 (bits 4-15) | row in the tile (bits 16-31)
 constexpr uint32_t kLdsRecWords = kLdsQueues;
-constexpr uint32_t kLdsRecMeta = kLdsRecWords + (kHotLanes / 64) * kRecCap * 16;
+constexpr uint32_t kLdsRecMeta = kLdsRecWords + kHotWaves * kRecCap * 16;
 // fused step: the workgroup's 12 u64 totals (3 per range)
-constexpr uint32_t kLdsTotals = (kLdsRecMeta + (kHotLanes / 64) * kRecCap * 4 + 7u) & ~7u;
+constexpr uint32_t kLdsTotals = (kLdsRecMeta + kHotWaves * kRecCap * 4 + 7u) & ~7u;
 // + the last-workgroup flag; then the workgroup's exact-path word count and
 // its waves-done count
 constexpr uint32_t kLdsWords = kLdsTotals + 12 * 8 + 8;
@@ -85,7 +90,7 @@ constexpr uint32_t kLdsWords = kLdsTotals + 12 * 8 + 8;
 constexpr uint32_t kLdsUnits = kLdsWords + 8;
 constexpr uint32_t kLdsBytes = kLdsUnits + 4;
 static_assert(kLdsBytes <= 160 * 1024, "chroma kernel LDS image");
-static_assert((kRecCap * 16) % 16 == 0 && kRecCap >= 64 + 8, "record queue");
+static_assert((kRecCap * 16) % 16 == 0 && kRecCap >= 64 + 4, "record queue");
 
 typedef __attribute__((address_space(3))) uint8_t* lds8_t;
 typedef __attribute__((address_space(3))) uint16_t* lds16_t;
@@ -564,6 +569,7 @@ struct ChromaGeom {
   // ceil(2^20 / cpr), exact for lt < 1024 and cpr < 1024
   FastDiv fd_units, fd_tiles;
   uint32_t cpr_inv;
+  int32_t units;  // wave-sized units per tile: ceil(k * cpr / 64) <= kHotWaves
 };
 
 // The 12 per-lane values (3 per range, 4 ranges) summed over the wave: two
@@ -683,7 +689,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
   // 64 (u % U) ..), handed to the waves in order as they finish (a wave's
   // first unit is its own index): the waves of a SIMD with fewer waves run
   // faster and take more units, so the SIMDs end together.
-  const uint32_t U = blockDim.x >> 6;
+  const uint32_t U = (uint32_t)g.units;  // wave-sized units per tile
   const uint32_t n_units = (uint32_t)(t_end - t_begin) * U;
   for (uint32_t u = __builtin_amdgcn_readfirstlane(wave); u < n_units;) {  // (wave-uniform: SGPRs)
     uint32_t next = 0;
@@ -1003,7 +1009,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     }
     unpack_exc(acc);
     emit(acc);
-    u = __builtin_amdgcn_readfirstlane(next) + U;
+    u = __builtin_amdgcn_readfirstlane(next) + (blockDim.x >> 6);  // after the waves' first units
   }
   // the exact-path word count: per workgroup in LDS, one device atomic by its
   // last wave (AUTO's measured share, ChromaTables::flagged_words)
@@ -1206,7 +1212,7 @@ int launch_t(const KernelArgs& a, const ChromaGeom& g, const ChromaTables* ct, h
   hipError_t e = set_dynamic_lds(reinterpret_cast<const void*>(kern), (int)kLdsBytes);
   if (e != hipSuccess) return e;
   const int cus = device_cus();
-  const int block = ((g.k * g.cpr + 63) / 64) * 64;
+  const int block = 64 * kHotWaves;
   const int64_t grid = g.n_tiles < cus ? g.n_tiles : cus;  // one workgroup per CU (LDS image)
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(block), kLdsBytes, s, a, g, ct);
   return hipGetLastError();
@@ -1273,7 +1279,8 @@ bool chroma_geometry(const KernelArgs& a, ChromaGeom& g) {
   if (2LL * span > 65535) return false;
   int r = 65535 / (2 * span);
   g.flush_rounds = r > 127 ? 127 : r;
-  g.fd_units = make_div((uint32_t)((g.k * g.cpr + 63) / 64));  // the launch's waves per workgroup
+  g.units = (g.k * g.cpr + 63) / 64;
+  g.fd_units = make_div((uint32_t)g.units);
   g.fd_tiles = make_div((uint32_t)g.tiles_per_frame);
   g.cpr_inv = (uint32_t)(((1u << 20) + (uint32_t)cpr - 1) / (uint32_t)cpr);
   return true;
