@@ -72,6 +72,29 @@ def test_webcam_line_process_vs_oracle(hsv, oracle_mod, geom):
         s.close()
 
 
+@pytest.mark.parametrize("geom", [(640, 480, 1280, 320, 240, 640), (320, 240, 640, 160, 120, 320),
+                                  (320, 240, 640, 200, 150, 401)])
+def test_webcam_line_target_at_the_edges(hsv, oracle_mod, geom):
+    """A one-pixel line in the first or the last column: the target line's
+    columns cx - 1 .. cx + 1 are clamped to the frame (drawOutputPixelBound),
+    in the 2:1 pass that draws the overlay itself and in the separate one."""
+    w, h, ll, ow, oh, oll = geom
+    s = _sensor(hsv, w, h, ll, ow, oh, oll)
+    try:
+        for seed, x0 in ((11, 0), (12, w - 1), (13, 1), (14, w - 2)):
+            fr = oracle_mod.wline_scene(w, h, ll, seed, x0=x0, slope=0.0, line_w=1)
+            out = np.full(oh * oll, 0xCD, np.uint8)
+            rc, oa = s.process(fr, (0, 359, 0, 100, 0, 30), out_buffer=out)
+            assert rc == 0
+            rrc, ref, ref_pv, _ = oracle_mod.wline_run(fr, w, h, ll, 0, 30, out_width=ow, out_height=oh,
+                                                       out_line_length=oll)
+            assert rrc == 0 and abs(ref["target_x"]) >= 98  # the target at an edge
+            assert (oa.alg.targetX, oa.alg.targetY, oa.alg.targetSize) == _targets(ref), (geom, x0)
+            assert np.array_equal(out, ref_pv), (geom, x0)
+    finally:
+        s.close()
+
+
 def test_webcam_line_hue_and_sat_ignored(hsv, oracle_mod):
     """Only detectValFrom/To are read (LSEQW:345-351): any H/S in InArgs gives
     the same result."""

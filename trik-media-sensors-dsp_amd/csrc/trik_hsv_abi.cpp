@@ -338,6 +338,9 @@ struct TrikCvHandle {
   int maps_key[6] = {-1, -1, -1, -1, -1, -1};
   int32_t maps_rows2 = -1;  // first source row when the maps are the 2:1 ones, else -1
   int32_t maps_rows2_c0 = 0, maps_rows2_c1 = 0;  // the output columns the 2:1 maps write
+  // the line sensors' overlay geometry on these maps (PreviewArgs::ovl_*)
+  int32_t maps_ovl_ok = 0, maps_ovl_mag[4] = {-1, -1, -1, -1}, maps_ovl_band[2] = {-1, -1};
+  int32_t maps_ovl_c_lo = 0, maps_ovl_c_hi = -1;
   std::vector<uint32_t> h_maps;
   StreamUses maps_users;
 
@@ -865,6 +868,23 @@ int32_t ensure_maps(TrikCvHandle* h, int w, int hgt, int ow, int oh, hipStream_t
   h->maps_rows2 = rows2 ? (int32_t)last_row[0] : -1;
   h->maps_rows2_c0 = c0;
   h->maps_rows2_c1 = c1;
+  // the line overlays' output pixels (line_overlay_kernel, LSEQ:419-474): a
+  // column map with steps of 0 or 1 sends any source interval to one interval
+  const uint32_t* wi2wo = h->h_maps.data();
+  const uint32_t* hi2ho = wi2wo + w;
+  bool step1 = w > 0 && hgt > 0;
+  for (int c = 1; step1 && c < w; ++c) step1 = wi2wo[c] - wi2wo[c - 1] <= 1u;
+  h->maps_ovl_ok = step1 ? 1 : 0;
+  if (step1) {
+    const auto cl = [](int v, int n) { return v < 0 ? 0 : (v > n - 1 ? n - 1 : v); };
+    const int hw = w / 2, hh = hgt / 2, step = 40;
+    const int cols[4] = {hw - step, hw + step, hw - 2 * step, hw + 2 * step};
+    for (int j = 0; j < 4; ++j) h->maps_ovl_mag[j] = (int32_t)wi2wo[cl(cols[j], w)];
+    h->maps_ovl_band[0] = (int32_t)hi2ho[cl(hh, hgt)];
+    h->maps_ovl_band[1] = (int32_t)hi2ho[cl(hh + 2 * step, hgt)];
+    h->maps_ovl_c_lo = (int32_t)wi2wo[0];
+    h->maps_ovl_c_hi = (int32_t)wi2wo[w - 1];
+  }
   return 0;
 }
 
@@ -891,6 +911,12 @@ PreviewArgs preview_args(const TrikCvHandle* h, const TrikHsvFrameBatch& b,
   a.rows2_first = h->maps_rows2;
   a.rows2_c0 = h->maps_rows2_c0;
   a.rows2_c1 = h->maps_rows2_c1;
+  a.ovl_ok = h->maps_ovl_ok;
+  for (int j = 0; j < 4; ++j) a.ovl_mag[j] = h->maps_ovl_mag[j];
+  a.ovl_band[0] = h->maps_ovl_band[0];
+  a.ovl_band[1] = h->maps_ovl_band[1];
+  a.ovl_c_lo = h->maps_ovl_c_lo;
+  a.ovl_c_hi = h->maps_ovl_c_hi;
   return a;
 }
 
@@ -1439,8 +1465,7 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
             TableSet* set = nullptr;
             r = preview_tables(h, pa, line_alg(ia.detectValFrom, ia.detectValTo), h->stream, &set);
             if (r) return r;
-            HIP_TRY(launch_preview_body(pa, h->stream));
-            HIP_TRY(launch_line_overlay(pa, h->d_sums, h->stream));
+            HIP_TRY(launch_line_preview(pa, h->d_sums, 1, h->stream));
             r = note_uses(h, set, true, h->stream);
             if (r) return r;
             HIP_TRY(hipMemcpyAsync(out_ptr, h->d_preview, pb, hipMemcpyDeviceToHost, h->stream));
@@ -1472,8 +1497,7 @@ extern "C" int32_t TRIK_VIDTRANSCODE_CV_process(TRIK_VIDTRANSCODE_CV_Handle h,
             TableSet* set = nullptr;
             r = preview_tables(h, pa, wr, h->stream, &set);
             if (r) return r;
-            HIP_TRY(launch_preview_body(pa, h->stream));
-            HIP_TRY(launch_wline_overlay(pa, h->d_sums, h->stream));
+            HIP_TRY(launch_line_preview(pa, h->d_sums, 0, h->stream));
             r = note_uses(h, set, true, h->stream);
             if (r) return r;
             HIP_TRY(hipMemcpyAsync(out_ptr, h->d_preview, pb, hipMemcpyDeviceToHost, h->stream));
@@ -1830,8 +1854,7 @@ extern "C" int32_t trik_hsv_line_preview(TRIK_VIDTRANSCODE_CV_Handle h, const Tr
   TableSet* set = nullptr;
   rc = preview_tables(h, pa, line_alg(val_from, val_to), s, &set);
   if (rc) return rc;
-  HIP_TRY(launch_preview_body(pa, s));
-  HIP_TRY(launch_line_overlay(pa, sums, s));
+  HIP_TRY(launch_line_preview(pa, sums, 1, s));
   return note_uses(h, set, true, s);
 }
 

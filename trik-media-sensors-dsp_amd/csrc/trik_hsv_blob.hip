@@ -469,9 +469,12 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
   if (lane == 0 && a.n_labels) a.n_labels[f] = n;
 }
 
+template <bool LDSMAP>
 __global__ __launch_bounds__(64) void blob_overlay_kernel(PreviewArgs a, const int32_t* top) {
+  extern __shared__ uint32_t smaps[];
   const int f = blockIdx.x, lane = threadIdx.x;
-  const Canvas cv{a.previews + (int64_t)f * a.preview_stride, a.out_ll, a.width, a.height, a.wi2wo, a.hi2ho};
+  const Canvas cv = stage_canvas<LDSMAP>(smaps, a.previews + (int64_t)f * a.preview_stride, a.out_ll, a.width,
+                                         a.height, a.wi2wo, a.hi2ho, lane);
   draw_guides(cv, lane, 64);  // OSEQ:548-561
   __syncthreads();
   // drawFatPixel (OSEQ:92-108) per kept target, in target order: lane 9*i + j
@@ -551,7 +554,11 @@ int launch_blob(const BlobArgs& a, hipStream_t s) {
 
 int launch_blob_overlay(const PreviewArgs& a, const int32_t* top, hipStream_t s) {
   if (a.n_frames <= 0 || a.width <= 0 || a.height <= 0) return hipSuccess;
-  hipLaunchKernelGGL(blob_overlay_kernel, dim3((unsigned)a.n_frames), dim3(64), 0, s, a, top);
+  const size_t map_bytes = sizeof(uint32_t) * ((size_t)a.width + (size_t)a.height);
+  if (map_bytes <= kMapLdsBytes)
+    hipLaunchKernelGGL(blob_overlay_kernel<true>, dim3((unsigned)a.n_frames), dim3(64), map_bytes, s, a, top);
+  else
+    hipLaunchKernelGGL(blob_overlay_kernel<false>, dim3((unsigned)a.n_frames), dim3(64), 0, s, a, top);
   return hipGetLastError();
 }
 

@@ -209,6 +209,16 @@ struct PreviewArgs {
   // range 0 accepts every hue (its detect_mode() is not kDetectFull): the 2:1
   // kernel tests the sat&val mask alone
   int32_t hue_free = 0;
+  // The line sensors' overlays drawn by preview_rows2_kernel in the same pass
+  // (launch_line_preview; LSEQ:419-474, LSEQW:396-417 through
+  // drawOutputPixelBound), set when ovl_ok (the column map is monotone with
+  // steps of 0 or 1, so the output columns a source interval hits are one
+  // interval): magenta on output columns ovl_mag[] of every row, red on rows
+  // ovl_band[] (-1: none) over columns [ovl_c_lo, ovl_c_hi], and red on frame
+  // f's target columns wi2wo[clamp(cx - 1 .. cx + 1)] (ovl_sums[f].points > 10)
+  const TrikHsvTargetSums* ovl_sums = nullptr;
+  int32_t ovl_ok = 0;
+  int32_t ovl_mag[4] = {-1, -1, -1, -1}, ovl_band[2] = {-1, -1}, ovl_c_lo = 0, ovl_c_hi = -1;
 };
 
 // Auto HSV range of N frames (trik_hsv_operator.hip); out[f][6] = detectHue,
@@ -285,6 +295,11 @@ int launch_line_overlay(const PreviewArgs& a, const TrikHsvTargetSums* sums, hip
 int launch_wline_targets(int n_frames, int width, int height, const TrikHsvTargetSums* sums, TrikHsvTarget* targets,
                          hipStream_t s);
 int launch_wline_overlay(const PreviewArgs& a, const TrikHsvTargetSums* sums, hipStream_t s);
+// preview_rows2_kernel alone (hipErrorNotSupported where it does not apply)
+int launch_preview_rows2(const PreviewArgs& a, hipStream_t s);
+// a line sensor's whole preview: body and overlay (band = 1: the ov7670 line
+// sensor's band lines), fused into one pass where the 2:1 kernel applies
+int launch_line_preview(PreviewArgs a, const TrikHsvTargetSums* sums, int band, hipStream_t s);
 
 // ov7670 multi-blob sensor of N frames (trik_hsv_blob.hip).
 struct BlobArgs {

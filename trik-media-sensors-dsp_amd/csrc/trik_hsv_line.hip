@@ -344,4 +344,20 @@ int launch_line_overlay(const PreviewArgs& a, const TrikHsvTargetSums* sums, hip
   return hipGetLastError();
 }
 
+// The whole line-sensor preview: with the 2:1 maps the overlay is drawn by
+// preview_rows2_kernel in the same pass (the previews are written once);
+// otherwise the preview body, then line_overlay_kernel.
+int launch_line_preview(PreviewArgs a, const TrikHsvTargetSums* sums, int band, hipStream_t s) {
+  if (a.ovl_ok && sums) {
+    a.ovl_sums = sums;
+    if (!band) a.ovl_band[0] = a.ovl_band[1] = -1;
+    const int e = launch_preview_rows2(a, s);
+    if (e != hipErrorNotSupported) return e;
+    a.ovl_sums = nullptr;
+  }
+  const int e = launch_preview_body(a, s);
+  if (e != hipSuccess) return e;
+  return band ? launch_line_overlay(a, sums, s) : launch_wline_overlay(a, sums, s);
+}
+
 }  // namespace trik_hsv

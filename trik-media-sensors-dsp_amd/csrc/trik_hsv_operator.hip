@@ -198,7 +198,10 @@ struct PreviewRowsGeom {
   uint32_t step_f, step_r, step_q;  // the grid's lane count T as (frames, rows, groups)
 };
 constexpr int kRowsQ = 2;  // units per lane and round
-template <int LAYOUT, bool WIN, bool HUEFREE>
+constexpr uint32_t rgb565x(uint32_t rgb) {  // write_px565's value
+  return ((rgb >> 19) & 0x001fu) | ((rgb >> 5) & 0x07e0u) | ((rgb << 8) & 0xf800u);
+}
+template <int LAYOUT, bool WIN, bool HUEFREE, bool OVL = false>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8)))
 void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
   using namespace stripe_px;
@@ -260,6 +263,22 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
           ws[(2 * d + 1) % PX] = __builtin_amdgcn_perm(cc[d], yy[d], 0x0603070Cu);
         }
       }
+      // OVL: red columns [t_lo, t_hi] of this frame's target line (empty
+      // unless points > 10), red over [ovl_c_lo, ovl_c_hi] on a band row
+      uint32_t t_lo = 1u, t_hi = 0u;
+      bool band_row = false;
+      if (OVL) {
+        const TrikHsvTargetSums ts = a.ovl_sums[ff[u] < nf ? ff[u] : 0u];
+        const uint32_t n = (uint32_t)ts.points;
+        if (n > 10) {  // LSEQ:464-474: drawRgbTargetCenterLine(targetX), columns cx - 1 .. cx + 1
+          const int32_t cx = (int32_t)((uint32_t)(int32_t)ts.sum_x / n), wm = a.width - 1;
+          const int32_t c0 = cx - 1 < 0 ? 0 : (cx - 1 > wm ? wm : cx - 1);
+          const int32_t c1 = cx + 1 < 0 ? 0 : (cx + 1 > wm ? wm : cx + 1);
+          t_lo = a.wi2wo[c0];
+          t_hi = a.wi2wo[c1];
+        }
+        band_row = (int32_t)rr[u] == a.ovl_band[0] || (int32_t)rr[u] == a.ovl_band[1];
+      }
       uint32_t v[PX];
 #pragma unroll
       for (int k = 0; k < PX; ++k) {
@@ -281,6 +300,13 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
         const uint32_t c565 = ((uint32_t)p.r >> 3) | (((uint32_t)p.g & 0xFCu) << 3) | (((uint32_t)p.b & 0xF8u) << 8);
         v[k] = det ? 0xFFE0u : c565;
         if (WIN) v[k] = c >= (uint32_t)a.rows2_c0 && c < (uint32_t)a.rows2_c1 ? v[k] : 0u;
+        if (OVL) {  // thin lines (magenta) first, then the band and target lines (red) over them
+          const bool mag = (int32_t)c == a.ovl_mag[0] || (int32_t)c == a.ovl_mag[1] ||
+                           (int32_t)c == a.ovl_mag[2] || (int32_t)c == a.ovl_mag[3];
+          const bool red = (band_row && (int32_t)c >= a.ovl_c_lo && (int32_t)c <= a.ovl_c_hi) ||
+                           (c >= t_lo && c <= t_hi);
+          v[k] = red ? rgb565x(0xff0000u) : (mag ? rgb565x(0xff00ffu) : v[k]);
+        }
       }
       if (ff[u] < nf) {
         uint8_t* dst = a.previews + (int64_t)ff[u] * a.preview_stride + (int64_t)rr[u] * a.out_ll + 2 * PX * (int64_t)qq[u];
@@ -299,11 +325,13 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
 // One wave per frame.  All guide-line pixels have one colour and all circle
 // pixels another, so within each phase the write order is immaterial; only
 // "lines before circle" (WSEQ:476-494) is kept, by the barrier.
+template <bool LDSMAP>
 __global__ __launch_bounds__(64) void overlay_kernel(PreviewArgs a, const TrikHsvTargetSums* sums,
                                                      int sums_pitch) {
+  extern __shared__ uint32_t smaps[];
   const int f = blockIdx.x, lane = threadIdx.x;
-  const Canvas cv{a.previews + (int64_t)f * a.preview_stride, a.out_ll, a.width, a.height, a.wi2wo,
-                  a.hi2ho};
+  const Canvas cv = stage_canvas<LDSMAP>(smaps, a.previews + (int64_t)f * a.preview_stride, a.out_ll, a.width,
+                                         a.height, a.wi2wo, a.hi2ho, lane);
   draw_guides(cv, lane, 64);  // WSEQ:471-485
   __syncthreads();
   const TrikHsvTargetSums s = sums[(int64_t)f * sums_pitch];
@@ -498,7 +526,14 @@ static int launch_rows2(const PreviewArgs& a, hipStream_t s) {
   if (total >= (1ll << 31)) return hipErrorNotSupported;
   if (total == 0) return hipSuccess;
   const bool win = a.rows2_c0 > 0 || a.rows2_c1 < a.out_w, hue_free = a.hue_free && !a.meta;
+  const bool ovl = a.ovl_sums != nullptr;
+  if (ovl && (!a.ovl_ok || !hue_free)) return hipErrorNotSupported;  // the line sensors' previews only
   using Kern = void (*)(PreviewArgs, PreviewRowsGeom);
+  static const Kern ovl_kerns[2][2] = {
+      {preview_rows2_kernel<TRIK_HSV_LAYOUT_YUYV, false, true, true>,
+       preview_rows2_kernel<TRIK_HSV_LAYOUT_YUYV, true, true, true>},
+      {preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, false, true, true>,
+       preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, true, true, true>}};
   static const Kern kerns[2][2][2] = {
       {{preview_rows2_kernel<TRIK_HSV_LAYOUT_YUYV, false, false>, preview_rows2_kernel<TRIK_HSV_LAYOUT_YUYV, false, true>},
        {preview_rows2_kernel<TRIK_HSV_LAYOUT_YUYV, true, false>, preview_rows2_kernel<TRIK_HSV_LAYOUT_YUYV, true, true>}},
@@ -506,7 +541,7 @@ static int launch_rows2(const PreviewArgs& a, hipStream_t s) {
         preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, false, true>},
        {preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, true, false>,
         preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, true, true>}}};
-  const Kern kern = kerns[yuyv ? 0 : 1][win ? 1 : 0][hue_free ? 1 : 0];
+  const Kern kern = ovl ? ovl_kerns[yuyv ? 0 : 1][win ? 1 : 0] : kerns[yuyv ? 0 : 1][win ? 1 : 0][hue_free ? 1 : 0];
   hipError_t e = set_dynamic_lds(reinterpret_cast<const void*>(kern), 80 * 1024);
   if (e != hipSuccess) return e;
   PreviewRowsGeom g;
@@ -558,6 +593,11 @@ static int launch_gather(const PreviewArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+int launch_preview_rows2(const PreviewArgs& a, hipStream_t s) {
+  if (a.n_frames <= 0 || a.out_w <= 0 || a.out_h <= 0) return hipSuccess;
+  return launch_rows2(a, s);
+}
+
 int launch_preview_body(const PreviewArgs& a, hipStream_t s) {
   if (a.n_frames <= 0 || a.out_w <= 0 || a.out_h <= 0) return hipSuccess;
   return launch_gather(a, s);
@@ -567,7 +607,11 @@ int launch_preview(const PreviewArgs& a, const TrikHsvTargetSums* sums, int sums
   if (a.n_frames <= 0 || a.out_w <= 0 || a.out_h <= 0) return hipSuccess;
   hipError_t e = (hipError_t)launch_gather(a, s);
   if (e != hipSuccess || a.width <= 0 || a.height <= 0) return e;
-  hipLaunchKernelGGL(overlay_kernel, dim3((unsigned)a.n_frames), dim3(64), 0, s, a, sums, sums_pitch);
+  const size_t map_bytes = sizeof(uint32_t) * ((size_t)a.width + (size_t)a.height);
+  if (map_bytes <= kMapLdsBytes)
+    hipLaunchKernelGGL(overlay_kernel<true>, dim3((unsigned)a.n_frames), dim3(64), map_bytes, s, a, sums, sums_pitch);
+  else
+    hipLaunchKernelGGL(overlay_kernel<false>, dim3((unsigned)a.n_frames), dim3(64), 0, s, a, sums, sums_pitch);
   return hipGetLastError();
 }
 

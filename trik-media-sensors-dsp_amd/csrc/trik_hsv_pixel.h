@@ -106,6 +106,21 @@ struct Canvas {
   }
 };
 
+// The preview scale maps (wi2wo then hi2ho, W + H contiguous words) staged
+// in LDS by one wave when they fit kMapLdsBytes: every drawn point looks up
+// both maps, and from LDS that lookup no longer waits on a global load.
+constexpr size_t kMapLdsBytes = 32 * 1024;
+template <bool LDSMAP>
+__device__ inline Canvas stage_canvas(uint32_t* smaps, uint8_t* out, int out_ll, int width, int height,
+                                      const uint32_t* wi2wo, const uint32_t* hi2ho, int lane) {
+  if (LDSMAP) {
+    for (int i = lane; i < width + height; i += 64) smaps[i] = wi2wo[i];
+    __syncthreads();
+    return Canvas{out, out_ll, width, height, smaps, smaps + width};
+  }
+  return Canvas{out, out_ll, width, height, wi2wo, hi2ho};
+}
+
 // The 8 magenta guide lines of the object sensors (WSEQ:136-166,471-485;
 // OSEQ:227-255,548-561): 4 vertical and 4 horizontal lines of 2 x 100 points
 // around the centre, step = H/6; one colour, so any lane order.
