@@ -339,7 +339,7 @@ struct TrikCvHandle {
   int32_t maps_rows2 = -1;  // first source row when the maps are the 2:1 ones, else -1
   int32_t maps_rows2_c0 = 0, maps_rows2_c1 = 0;  // the output columns the 2:1 maps write
   // the line sensors' overlay geometry on these maps (PreviewArgs::ovl_*)
-  int32_t maps_ovl_ok = 0, maps_ovl_mag[4] = {-1, -1, -1, -1}, maps_ovl_band[2] = {-1, -1};
+  int32_t maps_ovl_half = 0, maps_ovl_ok = 0, maps_ovl_mag[4] = {-1, -1, -1, -1}, maps_ovl_band[2] = {-1, -1};
   int32_t maps_ovl_c_lo = 0, maps_ovl_c_hi = -1;
   std::vector<uint32_t> h_maps;
   StreamUses maps_users;
@@ -875,6 +875,9 @@ int32_t ensure_maps(TrikCvHandle* h, int w, int hgt, int ow, int oh, hipStream_t
   bool step1 = w > 0 && hgt > 0;
   for (int c = 1; step1 && c < w; ++c) step1 = wi2wo[c] - wi2wo[c - 1] <= 1u;
   h->maps_ovl_ok = step1 ? 1 : 0;
+  bool half = step1;
+  for (int c = 0; half && c < w; ++c) half = wi2wo[c] == (uint32_t)c >> 1;
+  h->maps_ovl_half = half ? 1 : 0;
   if (step1) {
     const auto cl = [](int v, int n) { return v < 0 ? 0 : (v > n - 1 ? n - 1 : v); };
     const int hw = w / 2, hh = hgt / 2, step = 40;
@@ -912,6 +915,7 @@ PreviewArgs preview_args(const TrikCvHandle* h, const TrikHsvFrameBatch& b,
   a.rows2_c0 = h->maps_rows2_c0;
   a.rows2_c1 = h->maps_rows2_c1;
   a.ovl_ok = h->maps_ovl_ok;
+  a.ovl_half = h->maps_ovl_half;
   for (int j = 0; j < 4; ++j) a.ovl_mag[j] = h->maps_ovl_mag[j];
   a.ovl_band[0] = h->maps_ovl_band[0];
   a.ovl_band[1] = h->maps_ovl_band[1];

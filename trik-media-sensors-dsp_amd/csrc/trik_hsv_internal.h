@@ -217,7 +217,7 @@ struct PreviewArgs {
   // ovl_band[] (-1: none) over columns [ovl_c_lo, ovl_c_hi], and red on frame
   // f's target columns wi2wo[clamp(cx - 1 .. cx + 1)] (ovl_sums[f].points > 10)
   const TrikHsvTargetSums* ovl_sums = nullptr;
-  int32_t ovl_ok = 0;
+  int32_t ovl_ok = 0, ovl_half = 0;  // ovl_half: wi2wo[c] = c / 2 for every c
   int32_t ovl_mag[4] = {-1, -1, -1, -1}, ovl_band[2] = {-1, -1}, ovl_c_lo = 0, ovl_c_hi = -1;
 };
 

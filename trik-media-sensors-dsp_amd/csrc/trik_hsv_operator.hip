@@ -236,7 +236,7 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
     f += g.step_f + (cr ? 1u : 0u);
   };
   while (f < nf) {
-    uint32_t ff[kRowsQ], rr[kRowsQ], qq[kRowsQ];
+    uint32_t ff[kRowsQ], rr[kRowsQ], qq[kRowsQ], tpts[kRowsQ], tsx[kRowsQ];
     u32x4 w[kRowsQ], wc[kRowsQ];
 #pragma unroll
     for (int u = 0; u < kRowsQ; ++u) {
@@ -244,6 +244,11 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
       rr[u] = r;
       qq[u] = q;
       const uint32_t fl = f < nf ? f : 0u;  // past the end: re-read frame 0, not stored
+      if (OVL) {  // the low words of points and sumX, loaded with the frame's
+        const uint32_t* ts = reinterpret_cast<const uint32_t*>(a.ovl_sums + fl);
+        tpts[u] = ts[0];
+        tsx[u] = ts[2];
+      }
       const uint8_t* src = a.frames + (int64_t)fl * a.frame_stride +
                            (int64_t)((uint32_t)a.rows2_first + 2u * r) * a.line_length + 16 * (int64_t)q;
       w[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
@@ -268,14 +273,14 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
       uint32_t t_lo = 1u, t_hi = 0u;
       bool band_row = false;
       if (OVL) {
-        const TrikHsvTargetSums ts = a.ovl_sums[ff[u] < nf ? ff[u] : 0u];
-        const uint32_t n = (uint32_t)ts.points;
+        const uint32_t n = tpts[u];
         if (n > 10) {  // LSEQ:464-474: drawRgbTargetCenterLine(targetX), columns cx - 1 .. cx + 1
-          const int32_t cx = (int32_t)((uint32_t)(int32_t)ts.sum_x / n), wm = a.width - 1;
+          const int32_t cx = (int32_t)(tsx[u] / n), wm = a.width - 1;
           const int32_t c0 = cx - 1 < 0 ? 0 : (cx - 1 > wm ? wm : cx - 1);
           const int32_t c1 = cx + 1 < 0 ? 0 : (cx + 1 > wm ? wm : cx + 1);
-          t_lo = a.wi2wo[c0];
-          t_hi = a.wi2wo[c1];
+          // ovl_half: wi2wo[c] = c / 2 (the 2:1 maps), no dependent map loads
+          t_lo = a.ovl_half ? (uint32_t)c0 >> 1 : a.wi2wo[c0];
+          t_hi = a.ovl_half ? (uint32_t)c1 >> 1 : a.wi2wo[c1];
         }
         band_row = (int32_t)rr[u] == a.ovl_band[0] || (int32_t)rr[u] == a.ovl_band[1];
       }
