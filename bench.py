@@ -67,10 +67,11 @@ def parse():
     ap.add_argument("--targets", type=int, default=None)
     ap.add_argument("--kind", type=int, default=0, help="0 uniform random bytes, 1 scene")
     ap.add_argument("--cpu-frames-all", type=int, default=4096,
-                    help="CPU baseline sample on every allowed hardware thread (frames)")
-    ap.add_argument("--cpu-frames", type=int, default=1024, help="CPU sample on the per-GPU CPU share (frames)")
-    ap.add_argument("--scene-launches", type=int, default=20,
-                    help="launches timed on scene frames before the warmup (0: none)")
+                    help="CPU baseline sample on the job's CPUs (the cgroup quota, else every allowed thread)")
+    ap.add_argument("--cpu-frames", type=int, default=1024,
+                    help="CPU sample on every allowed thread when that exceeds the quota (oversubscribed)")
+    ap.add_argument("--scene-launches", type=int, default=60,
+                    help="launches timed on scene frames right before the warmup (0: none)")
     ap.add_argument("--cpu-frames-1core", type=int, default=64, help="single-thread CPU sample")
     ap.add_argument("--cpu-frames-emul", type=int, default=32,
                     help="sample of the oracle's intrinsic-level emulation (secondary rate)")
@@ -96,10 +97,11 @@ def cpu_baseline(args, width, height, ll, n_ranges, host, gpu_sums):
     batch's bytes): the clean-room scalar restatement of the path
     (oracle/trik_cpu_baseline.c, a plain CPU port: closed-form arithmetic,
     frames over POSIX threads), checked against the GPU sums of those frames.
-    `value`: every hardware thread this process may run on (SURVEY 8(d):
-    hardware_concurrency over the affinity mask); beside it the box's per-GPU
-    CPU share (OMP_NUM_THREADS, 16 on the bench box), one thread, and the
-    oracle's intrinsic-level emulation."""
+    `value` and `cores`: the CPUs this job actually gets -- the cgroup's CPU
+    quota when one is set (16 per GPU on the bench box), else every hardware
+    thread of the affinity mask.  Beside it: every allowed
+    thread when that is more than the quota (time-sliced, labelled
+    oversubscribed), one thread, and the oracle's intrinsic-level emulation."""
     import numpy as np
 
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -110,7 +112,8 @@ def cpu_baseline(args, width, height, ll, n_ranges, host, gpu_sums):
         allowed = len(os.sched_getaffinity(0))
     except AttributeError:
         allowed = machine
-    share = max(1, min(allowed, int(os.environ.get("OMP_NUM_THREADS", allowed))))
+    quota = cgroup_cpus()
+    cores = max(1, min(allowed, int(quota))) if quota else allowed
     rs = RANGES[:n_ranges]
     fb = height * ll
     px = width * height
@@ -120,28 +123,35 @@ def cpu_baseline(args, width, height, ll, n_ranges, host, gpu_sums):
         out = oracle.cpu_batch(host, fb, n, width, height, ll, oracle.LAYOUT_YUYV, rs, n_threads=threads)
         return out, time.perf_counter() - t0
 
-    n_all = min(args.cpu_frames_all, args.frames)
-    sums_all, dt_all = run(n_all, allowed)
-    n = min(args.cpu_frames, args.frames)
-    sums, dt = run(n, share)
-    n1 = min(args.cpu_frames_1core, n)
+    n_main = min(args.cpu_frames_all, args.frames)
+    sums_main, dt_main = run(n_main, cores)
+    checks = [(sums_main, n_main)]
+    out = {"value": round(n_main * px / dt_main / 1e6, 3), "unit": "Mpix/s", "cores": cores, "kind": "port",
+           "port": "clean-room scalar C restatement (oracle/trik_cpu_baseline.c), POSIX threads",
+           "sample": f"{n_main} frames x {width}x{height} YUYV, {n_ranges} ranges "
+                     f"(frames 0..{n_main - 1} of the GPU batch), {cores} threads, {dt_main:.2f} s",
+           "cores_source": ("the cgroup CPU quota" if quota else "the affinity mask (no cgroup quota)")}
+    if allowed > cores:  # every allowed thread, beyond the quota: time-sliced
+        n_all = min(args.cpu_frames, args.frames)
+        sums_all, dt_all = run(n_all, allowed)
+        checks.append((sums_all, n_all))
+        out["value_all_threads"] = round(n_all * px / dt_all / 1e6, 3)
+        out["all_threads"] = allowed
+        out["all_threads_note"] = (f"{n_all} frames on all {allowed} allowed threads, {dt_all:.2f} s: "
+                                   f"oversubscribed (the job's quota is {quota} CPUs), not the baseline")
+    n1 = min(args.cpu_frames_1core, n_main)
     _, dt1 = run(n1, 1)
-    ne = min(args.cpu_frames_emul, n)
+    ne = min(args.cpu_frames_emul, n_main)
     t2 = time.perf_counter()
-    emul, _ = oracle.batch(host, fb, ne, width, height, ll, oracle.LAYOUT_YUYV, rs, n_threads=share)
+    emul, _ = oracle.batch(host, fb, ne, width, height, ll, oracle.LAYOUT_YUYV, rs, n_threads=cores)
     dt2 = time.perf_counter() - t2
-    parity = (bool(np.array_equal(sums_all, gpu_sums[:n_all])) and bool(np.array_equal(sums, gpu_sums[:n]))
-              and bool(np.array_equal(emul, gpu_sums[:ne])))
-    return {"value": round(n_all * px / dt_all / 1e6, 3), "unit": "Mpix/s", "cores": allowed, "kind": "port",
-            "port": "clean-room scalar C restatement (oracle/trik_cpu_baseline.c), POSIX threads",
-            "sample": f"{n_all} frames x {width}x{height} YUYV, {n_ranges} ranges "
-                      f"(frames 0..{n_all - 1} of the GPU batch), {allowed} threads, {dt_all:.2f} s",
-            "value_share": round(n * px / dt / 1e6, 3), "share_threads": share,
-            "share_sample": f"{n} frames, {share} threads (the box's CPU share per GPU), {dt:.2f} s",
-            "value_1core": round(n1 * px / dt1 / 1e6, 3),
-            "machine_threads": machine, "threads_allowed": allowed, "cgroup_cpu_quota": cgroup_cpus(),
-            "value_intrinsic_emulation": round(ne * px / dt2 / 1e6, 3),
-            "cpu_model": cpu_model()}, parity
+    checks.append((emul, ne))
+    parity = all(bool(np.array_equal(got, gpu_sums[:n])) for got, n in checks)
+    out.update({"value_1core": round(n1 * px / dt1 / 1e6, 3),
+                "machine_threads": machine, "threads_allowed": allowed, "cgroup_cpu_quota": quota,
+                "value_intrinsic_emulation": round(ne * px / dt2 / 1e6, 3),
+                "cpu_model": cpu_model()})
+    return out, parity
 
 
 def cgroup_cpus():
@@ -214,7 +224,7 @@ def main():
     import torch.distributed as dist
 
     import trik_hsv
-    from trik_hsv.shard import all_reduce_totals, frame_shard
+    from trik_hsv.shard import all_reduce_totals, batch_totals, frame_shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -284,27 +294,6 @@ def main():
     # the first call of a fresh handle: table memory allocated, range tables
     # compiled on the host and uploaded, chroma-run tables built on the device
     first_ms, first_host_ms = timed_call(ranges)
-    # scene frames: camera-like content, the same step
-    scene = None
-    if args.scene_launches > 0 and not args.no_extras:
-        sframes = torch.empty_like(frames)
-        trik_hsv.synth(sframes, W, H, ll, trik_hsv.LAYOUT_YUYV, 1, SEED, first_frame=first)
-        full_step(sframes, ranges)
-        sev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(args.scene_launches)]
-        torch.cuda.synchronize()
-        for a, b in sev:
-            full_step(sframes, ranges, a, b)
-        torch.cuda.synchronize()
-        scene_ms = sorted(a.elapsed_time(b) for a, b in sev)
-        scene_avg = sum(scene_ms) / len(scene_ms)
-        del sframes
-        scene = {"kernel_ms": round(scene_avg, 4), "kernel_ms_median": round(scene_ms[len(scene_ms) // 2], 4),
-                 "frac": round(F * fb / (scene_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                 "mpix_per_s": round(F * W * H / (scene_avg / 1e3) / 1e6, 1), "launches": args.scene_launches,
-                 "data": "synthetic: device scene generator (gradients + 6 discs), seed 0x7A1C",
-                 "note": "the same full step on scene frames, timed before the warmup (not in `value`)"}
-
     # range sets the handle has not seen, on a warm handle (its table slots
     # already allocated): what a workload that changes ranges pays per change;
     # three new sets, each timed cold and then again (its steady cost), the
@@ -324,6 +313,33 @@ def main():
         cold_pairs.sort(key=lambda p: p[0] - p[1])
         new_ms, warm_ms, new_host_ms = cold_pairs[len(cold_pairs) // 2]
         timed_call(ranges)  # back to the bench set (rebuilt)
+    full_step(frames, ranges)
+    # scene frames: camera-like content, the same step.
+    # Last before the warmup, back to back: the timed steps then start from
+    # the clocks of a running workload, not from the power controller's
+    # transient after the idle gaps above (profiles/r04a_driver_cmd_launches.txt:
+    # the same launch ran 478-700 us across those phases)
+    scene = None
+    if args.scene_launches > 0 and not args.no_extras:
+        sframes = torch.empty_like(frames)
+        trik_hsv.synth(sframes, W, H, ll, trik_hsv.LAYOUT_YUYV, 1, SEED, first_frame=first)
+        full_step(sframes, ranges)
+        sev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.scene_launches)]
+        torch.cuda.synchronize()
+        for a, b in sev:
+            full_step(sframes, ranges, a, b)
+        torch.cuda.synchronize()
+        scene_ms = sorted(a.elapsed_time(b) for a, b in sev)
+        scene_avg = sum(scene_ms) / len(scene_ms)
+        del sframes
+        scene = {"kernel_ms": round(scene_avg, 4), "kernel_ms_median": round(scene_ms[len(scene_ms) // 2], 4),
+                 "frac": round(F * fb / (scene_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                 "mpix_per_s": round(F * W * H / (scene_avg / 1e3) / 1e6, 1), "launches": args.scene_launches,
+                 "data": "synthetic: device scene generator (gradients + 6 discs), seed 0x7A1C",
+                 "note": "the same full step on scene frames, timed back to back right before the warmup "
+                         "(not in `value`)"}
+
     # --- the timed steps ----------------------------------------------------
     for _ in range(args.warmup):
         step()
@@ -345,13 +361,21 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+    # what the timed steps reduced: the totals after the last step against a
+    # fresh sum of this rank's per-frame sums, reduced the same way
+    fresh = batch_totals(sums)
+    if backend == "nccl":
+        all_reduce_totals(fresh)
+    elif world > 1:
+        fresh = all_reduce_totals(fresh.cpu()).to(dev)
+    totals_ok = bool(torch.equal(fresh, totals))
+    ranks = dist.get_world_size() if world > 1 else 1
     kind = det.last_hot_kernel()
     kname = {trik_hsv.HOT_CHROMA: "chroma_kernel", trik_hsv.HOT_STRIPE: "stripe_kernel",
              trik_hsv.HOT_GENERIC: "reduce_kernel", trik_hsv.HOT_MIXED: "mixed"}.get(kind, "?")
-    cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    fused = kind == trik_hsv.HOT_CHROMA and F >= 4 * cus
+    fused = kind == trik_hsv.HOT_CHROMA  # the chroma-run kernel runs the whole step (chroma_fused_ok)
 
-    el = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    el = torch.tensor([elapsed, kern_ms, 0.0 if totals_ok else 1.0], dtype=torch.float64, device=dev)
     if world > 1:
         if backend == "nccl":
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -360,6 +384,7 @@ def main():
             dist.all_reduce(host, op=dist.ReduceOp.MAX)
             el.copy_(host)
     elapsed, kern_ms_max = float(el[0]), float(el[1])
+    totals_ok = float(el[2]) == 0.0  # on every rank
 
     px_total = total * W * H * args.steps
     value = px_total / elapsed / 1e6
@@ -371,7 +396,12 @@ def main():
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "strong" if args.total_frames else "weak", "vs_baseline": None,
-        "dtype": "u8",
+        "dtype": "u8", "ranks": ranks, "backend": (("nccl (RCCL)" if backend == "nccl" else backend)
+                                                  if world > 1 else "none (one process)"),
+        "totals_check": {"ok": totals_ok, "frames_reduced": total,
+                         "points": [int(x) for x in totals[:, 0].tolist()],
+                         "how": "after the timed steps, a fresh sum of the rank's per-frame sums, "
+                                "all-reduced over the same backend, equals the totals the steps reduced"},
         "data": "synthetic: device SplitMix64 uniform bytes, seed 0x7A1C" if args.kind == 0
                 else "synthetic: device scene generator (gradients + 6 discs), seed 0x7A1C",
         "config": {"workload": workload_name(args.workload, F, total, world, W, H, T),
@@ -398,8 +428,8 @@ def main():
                                "compiled and built on the device, then the hot kernel); "
                                "table_build_ms = cold_batch_ms - the same set's next step, the median "
                                "over three new sets (sets_ms: [cold, next] each); first_call: a fresh "
-                               "handle, table memory allocated too; measured before the warmup, after "
-                               "the scene block"}
+                               "handle, table memory allocated too; measured before the scene block and "
+                               "the warmup"}
     if scene is not None:
         out["scene"] = scene
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

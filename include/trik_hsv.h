@@ -521,8 +521,9 @@ int32_t trik_hsv_set_hot_kernel(TRIK_VIDTRANSCODE_CV_Handle handle, int32_t kind
  * readback if it is still in flight.  Returns 0 or TRIK_IVIDTRANSCODE_EFAIL. */
 int32_t trik_hsv_chroma_share(TRIK_VIDTRANSCODE_CV_Handle handle, double* share);
 /* The share of words the chroma-run kernel's exact path actually resolved on
- * the handle's recent AUTO batches of that range set (the maximum over its
- * groups; -1 before two readbacks have landed).  AUTO reads the kernel's
+ * the handle's recent batches of that range set that ran it (the maximum over
+ * its groups; -1 before two readbacks have landed; intervals with a batch on
+ * which the device chose the kernel are not measured).  AUTO reads the kernel's
  * counter back every few launches without waiting and sends a group whose
  * measured share exceeds TRIK_HSV_CHROMA_MAX_SHARE -- input concentrated on
  * the chromas its tables describe worst -- to the stripe kernel, trying the
@@ -530,7 +531,8 @@ int32_t trik_hsv_chroma_share(TRIK_VIDTRANSCODE_CV_Handle handle, double* share)
 int32_t trik_hsv_chroma_measured_share(TRIK_VIDTRANSCODE_CV_Handle handle, double* share);
 /* The kernel the handle's last hot call ran (TRIK_HSV_HOT_STRIPE, _CHROMA or
  * _GENERIC; TRIK_HSV_HOT_MIXED when its groups of 4 ranges ran different
- * kernels; 0 before any).  When the device chose (see above) this waits for
+ * kernels; 0 before any; a call with an empty batch launches nothing and
+ * leaves the answer unchanged).  When the device chose (see above) this waits for
  * the builder's readback. */
 int32_t trik_hsv_last_hot_kernel(TRIK_VIDTRANSCODE_CV_Handle handle);
 

@@ -69,6 +69,34 @@ def test_auto_moves_concentrated_input_to_stripe(torch_dev, hsv):
     det.close()
 
 
+def test_auto_measures_a_later_group(torch_dev, hsv):
+    """A first group of value-only ranges runs the stripe kernel's value form
+    under AUTO; the second group (the bench ranges) runs the chroma-run kernel.
+    Its measured share must still be read back and move it to the stripe
+    kernel on concentrated input (the readback used to count group
+    0's chroma-run launches only)."""
+    torch = torch_dev
+    n = 1024
+    frames = _exception_frames(torch, n)
+    vbands = [(0, 359, 0, 100, 10 + 20 * i, 20 + 20 * i) for i in range(4)]
+    ranges = vbands + list(BENCH_RANGES)
+    ref = hsv.Detector(hot=hsv.HOT_STRIPE)
+    want, _ = ref.process_batch(frames, W, H, LL, LAYOUT_YUYV, ranges)
+    torch.cuda.synchronize()
+    ref.close()
+    det = hsv.Detector()
+    ran = []
+    for _ in range(20):
+        sums, _ = det.process_batch(frames, W, H, LL, LAYOUT_YUYV, ranges)
+        torch.cuda.synchronize()
+        assert torch.equal(sums, want)
+        ran.append(det.last_hot_kernel())
+    assert ran[1] == hsv.HOT_MIXED, ran  # group 0 stripe (value form), group 1 chroma-run
+    assert det.chroma_measured_share() > 0.9
+    assert all(k == hsv.HOT_STRIPE for k in ran[-5:]), ran
+    det.close()
+
+
 def test_auto_keeps_uniform_input_on_chroma(torch_dev, hsv):
     torch = torch_dev
     n = 1024

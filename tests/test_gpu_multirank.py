@@ -98,6 +98,12 @@ def test_bench_two_ranks_rehearsal(extra):
     assert len(lines) == 1, r.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["value"] > 0
+    # the line proves what it measured: the process group's size, its backend,
+    # and the reduced totals equal to a fresh reduction of the per-frame sums
+    assert d["ranks"] == 2 and d["backend"] == "gloo"
+    chk = d["totals_check"]
+    assert chk["ok"] is True and chk["frames_reduced"] == d["config"]["frames_total"]
+    assert len(chk["points"]) == d["config"]["targets"] and all(p > 0 for p in chk["points"])
     if "--total-frames" in extra:
         assert d["scaling"] == "strong" and d["config"]["frames_total"] == 97
     else:

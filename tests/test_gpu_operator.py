@@ -158,6 +158,10 @@ def test_batch_auto_range_large_batch(hsv, oracle_mod, layout):
     (640, 480, 1280, 320, 240, 640, LAYOUT_YUYV, 0),
     (320, 240, 640, 200, 150, 401, LAYOUT_YUYV, 1),
     (320, 240, 320, 160, 120, 320, LAYOUT_OV7670, 1),
+    # square frames: 2:1 maps whose written columns end before out_w (the row
+    # kernel would load past the row; the gather takes them)
+    (480, 480, 960, 320, 240, 640, LAYOUT_YUYV, 1),
+    (240, 240, 240, 160, 120, 320, LAYOUT_OV7670, 1),
 ])
 def test_batch_preview(hsv, oracle_mod, w, h, ll, ow, oh, oll, layout, kind):
     import torch

@@ -258,6 +258,10 @@ struct TableSet {
     bool have_base = false;
     uint64_t launched = 0;      // words launched on the chroma-run kernel since the last readback
     uint64_t in_flight = 0;     // those of the readback in flight
+    // a gated launch (the device chose the kernel) since the last readback:
+    // its words may or may not be in the counter, so that interval is not
+    // measured (mixed) -- only the base moves
+    bool mixed = false, in_flight_mixed = false;
     double measured = -1.0;     // flagged words / words between the last two readbacks
     int stripe_runs = 0;        // batches sent to the stripe kernel by the measured share
   };
@@ -265,7 +269,7 @@ struct TableSet {
   unsigned long long* h_words = nullptr;  // pinned [groups_cap]: the readback
   hipEvent_t words_ready = nullptr;
   bool words_pending = false;
-  int chroma_runs = 0;  // AUTO chroma-run launches since the last readback
+  int chroma_runs = 0;  // calls with a chroma-run launch since the last readback
   void release() {
     users.wait_all();
     if (ready) (void)hipEventSynchronize(ready);
@@ -355,9 +359,13 @@ struct TrikCvHandle {
   TrikHsvTarget* d_targets = nullptr;
 
   // the chroma-run kernel's fused step: per-workgroup partial totals and the
-  // last-workgroup counter (0 between launches), shared by this handle's calls
+  // last-workgroup counter, per-frame accumulators and unit-done counts (all
+  // zero between launches), shared by this handle's calls
   unsigned long long* d_wg_part = nullptr;
   uint32_t* d_wg_cnt = nullptr;
+  unsigned long long* d_frame_acc = nullptr;
+  uint32_t* d_frame_done = nullptr;
+  int64_t frame_acc_cap = 0;  // frames
   StreamUses fused_users;
 
   // ov7670 multi-blob sensor: BitmapBuilder's sticky range (uninitialised in
@@ -393,6 +401,7 @@ void free_resources(TrikCvHandle* h) {
   h->fused_users.release();
   h->marks.release();
   (void)hipFree(h->d_wg_part);
+  (void)hipFree(h->d_frame_acc);
   (void)hipFree(h->d_frame);
   (void)hipFree(h->d_maps);
   (void)hipFree(h->d_preview);
@@ -418,6 +427,7 @@ void free_resources(TrikCvHandle* h) {
   h->d_blob_top = nullptr; h->d_blob_top_cap = 0;
   h->d_blob_targets = nullptr; h->d_blob_targets_cap = 0;
   h->d_wg_part = nullptr; h->d_wg_cnt = nullptr;
+  h->d_frame_acc = nullptr; h->d_frame_done = nullptr; h->frame_acc_cap = 0;
   h->sums_set = h->pending_set = nullptr;
   h->alg_ready = false;
 }
@@ -620,10 +630,12 @@ void poll_measured(TableSet& t) {
   for (size_t g = 0; g < t.probes.size(); ++g) {
     TableSet::Probe& p = t.probes[g];
     const uint64_t v = t.h_words[g];
-    if (p.have_base && p.in_flight > 0) p.measured = (double)(v - p.base) / (double)p.in_flight;
+    if (p.have_base && p.in_flight > 0 && !p.in_flight_mixed)
+      p.measured = (double)(v - p.base) / (double)p.in_flight;
     p.base = v;
     p.have_base = true;
     p.in_flight = 0;
+    p.in_flight_mixed = false;
   }
   t.words_pending = false;
 }
@@ -664,7 +676,9 @@ int32_t probe_measured(TableSet& t, bool reprobe, hipStream_t s) {
   HIP_TRY(hipEventRecord(t.words_ready, s));
   for (TableSet::Probe& p : t.probes) {
     p.in_flight = p.launched;
+    p.in_flight_mixed = p.mixed;
     p.launched = 0;
+    p.mixed = false;
   }
   t.words_pending = true;
   t.chroma_runs = 0;
@@ -690,16 +704,36 @@ int32_t note_uses(TrikCvHandle* h, TableSet* set, bool maps, hipStream_t s, Stre
   return 0;
 }
 
-// The fused step's scratch (one slot of 12 totals per CU, the counter zeroed
-// once), allocated on first use.
-int32_t ensure_fused_scratch(TrikCvHandle* h, hipStream_t s) {
-  if (h->d_wg_part) return 0;
-  const size_t parts = (size_t)device_cus() * 12;
-  void* p = nullptr;
-  HIP_TRY(hipMalloc(&p, sizeof(unsigned long long) * parts + 16));
-  h->d_wg_part = static_cast<unsigned long long*>(p);
-  h->d_wg_cnt = reinterpret_cast<uint32_t*>(h->d_wg_part + parts);
-  HIP_TRY(hipMemsetAsync(h->d_wg_cnt, 0, 16, s));
+// The fused step's scratch, allocated on first use: one slot of 12 totals per
+// CU and the last-workgroup counter; per frame a 128-byte accumulator (its
+// own cache line) and a unit-done count.  All zeroed once; every launch leaves
+// them zero.  A larger batch reallocates the per-frame part (after the
+// launches still using it: the caller ordered s after them).
+int32_t ensure_fused_scratch(TrikCvHandle* h, int64_t n_frames, hipStream_t s) {
+  if (!h->d_wg_part) {
+    const size_t parts = (size_t)device_cus() * 12;
+    void* p = nullptr;
+    HIP_TRY(hipMalloc(&p, sizeof(unsigned long long) * parts + 16));
+    h->d_wg_part = static_cast<unsigned long long*>(p);
+    h->d_wg_cnt = reinterpret_cast<uint32_t*>(h->d_wg_part + parts);
+    HIP_TRY(hipMemsetAsync(h->d_wg_cnt, 0, 16, s));
+  }
+  if (n_frames > h->frame_acc_cap) {
+    if (h->d_frame_acc) {
+      HIP_TRY(hipStreamSynchronize(s));
+      (void)hipFree(h->d_frame_acc);
+      h->d_frame_acc = nullptr;
+      h->frame_acc_cap = 0;
+    }
+    const int64_t cap = n_frames < 1024 ? 1024 : n_frames;
+    const size_t bytes = (size_t)cap * (128 + 4);
+    void* p = nullptr;
+    HIP_TRY(hipMalloc(&p, bytes));
+    HIP_TRY(hipMemsetAsync(p, 0, bytes, s));
+    h->d_frame_acc = static_cast<unsigned long long*>(p);
+    h->d_frame_done = reinterpret_cast<uint32_t*>(h->d_frame_acc + 16 * cap);
+    h->frame_acc_cap = cap;
+  }
   return 0;
 }
 
@@ -754,14 +788,15 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
     fused = fused && plans[g] == kPlanChroma && chroma_fused_ok(a);
   }
   if (fused) {
-    rc = ensure_fused_scratch(h, s);
-    if (rc) return rc;
     HIP_TRY(h->fused_users.order_after(s));
+    rc = ensure_fused_scratch(h, b->n_frames, s);
+    if (rc) return rc;
   }
   if (step && !fused && b->n_frames > 0 && sums)  // (frames of zero width or height: zero sums)
     HIP_TRY(hipMemsetAsync(sums, 0, sizeof(TrikHsvTargetSums) * (size_t)b->n_frames * n, s));
-  bool gated = false;
-  h->hot_groups.assign(groups, 0);
+  bool gated = false, chroma_ran = false;
+  // (an empty batch launches nothing and keeps the last call's answer)
+  if (!args.empty()) h->hot_groups.assign(groups, 0);
   for (size_t g = 0; g < args.size(); ++g) {
     KernelArgs& a = args[g];
     const HotPlan plan = plans[g];
@@ -773,14 +808,16 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
         a.totals = step->totals;
         a.wg_part = h->d_wg_part;
         a.wg_cnt = h->d_wg_cnt;
+        a.frame_acc = h->d_frame_acc;
+        a.frame_done = h->d_frame_done;
       }
       e = launch_chroma(a, t->d_chroma + g, masks != nullptr, s);
       if (e == hipSuccess) {
         h->hot_groups[g] = TRIK_HSV_HOT_CHROMA;
-        if (h->hot.load() == TRIK_HSV_HOT_AUTO) {
-          t->probes[g].launched += (uint64_t)a.n_frames * (uint64_t)(a.width / 2) * (uint64_t)a.height;
-          if (g == 0) ++t->chroma_runs;
-        }
+        // every chroma-run launch adds to the group's flagged_words (forced or
+        // AUTO), so every one counts its words: the two sides of the share
+        t->probes[g].launched += (uint64_t)a.n_frames * (uint64_t)(a.width / 2) * (uint64_t)a.height;
+        chroma_ran = true;
       }
     } else if (plan == kPlanGated) {
       // AUTO's rule on the device: the chroma-run kernel runs while this
@@ -803,6 +840,7 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
         }
         HIP_TRY(e);  // never an ungated launch after a gated one
         h->hot_groups[g] = (int8_t)-partner;
+        t->probes[g].mixed = true;
         gated = true;
         continue;
       }
@@ -818,6 +856,7 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
     HIP_TRY(e);
   }
   h->pending_set = gated ? t : nullptr;
+  if (chroma_ran) ++t->chroma_runs;  // once per call, whichever groups ran it
   if (!masks) {
     rc = probe_measured(*t, reprobe, s);
     if (rc) return rc;

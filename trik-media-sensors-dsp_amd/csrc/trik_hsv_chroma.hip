@@ -651,19 +651,16 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
       *(lds8_t)(uintptr_t)(kLdsVal + i) = a.tables->vmask[i];
     }
   }
-  // fused step: this workgroup's frames [f_first, f_end) (whole frames), its
-  // tiles; their sums zeroed here (no other workgroup adds to them: the
-  // stores reach L2 before this workgroup's first atomic, see the wait)
-  const int64_t f_first = a.fused ? (int64_t)a.n_frames * blockIdx.x / gridDim.x : 0;
-  const int64_t f_end = a.fused ? (int64_t)a.n_frames * (blockIdx.x + 1) / gridDim.x : 0;
-  const int64_t t_begin = a.fused ? f_first * g.tiles_per_frame : g.n_tiles * blockIdx.x / gridDim.x;
-  const int64_t t_end = a.fused ? f_end * g.tiles_per_frame : g.n_tiles * (blockIdx.x + 1) / gridDim.x;
-  if (a.fused) {
-    for (int64_t i = t; i < (f_end - f_first) * NR; i += blockDim.x)
-      a.sums[(f_first + i / NR) * a.sums_ranges + a.range_offset + i % NR] = TrikHsvTargetSums{0, 0, 0};
-    if (t < 12) st_u64(kLdsTotals + 8 * t, 0ull);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
+  // This workgroup's units: an even share of the batch's wave-sized units
+  // (unit u: tile u / U, lanes 64 (u % U) ..), whatever the frame boundaries
+  // (a frame's units may lie in several workgroups: the fused step counts
+  // them done per frame)
+  const uint32_t U = (uint32_t)g.units;                    // wave-sized units per tile
+  const uint32_t n_units_all = (uint32_t)(g.n_tiles * U);  // (< 2^32: chroma_geometry)
+  const uint32_t u_begin = (uint32_t)((uint64_t)n_units_all * blockIdx.x / gridDim.x);
+  const uint32_t u_end = (uint32_t)((uint64_t)n_units_all * (blockIdx.x + 1) / gridDim.x);
+  const uint32_t upf = U * (uint32_t)g.tiles_per_frame;   // units per frame
+  if (a.fused && t < 12) st_u64(kLdsTotals + 8 * t, 0ull);
   if (t < 3) *(lds32_t)(uintptr_t)(kLdsWords + 4 * t) = 0u;
   __syncthreads();
 
@@ -685,24 +682,63 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
   const uint32_t meta_b = ((SPLIT ? dx >> 3 : 1u) << 4) + ((uint32_t)half << 16);
 
   uint32_t resolved = 0;  // words this wave's exact path resolved (wave-uniform)
-  // Units: a tile's lanes in wave-sized groups (unit u: tile u / U, lanes
-  // 64 (u % U) ..), handed to the waves in order as they finish (a wave's
+  // The fused step's per-frame completion (wave-uniform): a unit's sums go
+  // to its frame's accumulator by device atomics, which execute at the memory
+  // side; once they are performed (this wave's vmcnt wait at its NEXT unit's
+  // end, when they long have been) the unit counts itself done on the
+  // frame's counter, and the count that counter returned is examined at the
+  // unit end after that (its latency hides behind a unit's loads).  The wave
+  // that counts a frame's last unit finalizes it.
+  int32_t pend_f = -1;  // frame of this wave's last emitted unit, not counted yet
+  int32_t chk_f = -1;   // frame whose count was issued, not examined yet
+  uint32_t chk_r = 0;   // lane 0: that count's value before this wave's add
+  // the frame's sums (exchanged for zero: the accumulator is clean for the
+  // next launch), its targets (WSEQ:486-505), its share of the totals
+  auto finalize = [&](int32_t F) {
+    unsigned long long* acc = a.frame_acc + 16 * (int64_t)F;
+    if (lane < NR) {
+      const uint64_t n = atomicExch(acc + 3 * lane, 0ull);
+      const uint64_t sx = atomicExch(acc + 3 * lane + 1, 0ull);
+      const uint64_t sy = atomicExch(acc + 3 * lane + 2, 0ull);
+      const int64_t o = (int64_t)F * a.sums_ranges + a.range_offset + lane;
+      a.sums[o] = TrikHsvTargetSums{(int64_t)n, (int64_t)sx, (int64_t)sy};
+      if (a.targets) a.targets[o] = target_of(n, sx, sy, a.width, a.height);
+      if (a.totals) {
+        lds_add_u64(kLdsTotals + 24u * (uint32_t)lane, n);
+        lds_add_u64(kLdsTotals + 24u * (uint32_t)lane + 8u, sx);
+        lds_add_u64(kLdsTotals + 24u * (uint32_t)lane + 16u, sy);
+      }
+    }
+    if (lane == 0) __hip_atomic_store(a.frame_done + F, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto examine = [&]() {  // the count issued at the previous unit end
+    if (chk_f < 0) return;
+    if (__builtin_amdgcn_readfirstlane(chk_r) + 1u == upf) finalize(chk_f);
+    chk_f = -1;
+  };
+  auto count_done = [&]() {  // the last emitted unit, once its atomics are performed
+    if (pend_f < 0) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t r = 0;
+    if (lane == 0) r = atomicAdd(a.frame_done + pend_f, 1u);
+    chk_r = r;
+    chk_f = pend_f;
+    pend_f = -1;
+  };
+  // Units handed to the workgroup's waves in order as they finish (a wave's
   // first unit is its own index): the waves of a SIMD with fewer waves run
   // faster and take more units, so the SIMDs end together.
-  const uint32_t U = (uint32_t)g.units;  // wave-sized units per tile
-  const uint32_t n_units = (uint32_t)(t_end - t_begin) * U;
-  for (uint32_t u = __builtin_amdgcn_readfirstlane(wave); u < n_units;) {  // (wave-uniform: SGPRs)
+  for (uint32_t u = u_begin + __builtin_amdgcn_readfirstlane(wave); u < u_end;) {  // (wave-uniform: SGPRs)
     uint32_t next = 0;
     if (lane == 0) next = __hip_atomic_fetch_add((__attribute__((address_space(3))) uint32_t*)(uintptr_t)kLdsUnits,
                                                  1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     // (wave-uniform divisions by multiplication; the results are moved to
     // SGPRs, else everything derived from them stays in VGPRs)
     // (tile indices fit 32 bits: chroma_geometry)
-    const uint32_t tl = __builtin_amdgcn_readfirstlane(fdiv(u, g.fd_units));
-    const uint32_t tile = (uint32_t)t_begin + tl;
+    const uint32_t tile = __builtin_amdgcn_readfirstlane(fdiv(u, g.fd_units));
     const int f = (int)__builtin_amdgcn_readfirstlane(fdiv(tile, g.fd_tiles));
     const int trem = (int)(tile - (uint32_t)f * (uint32_t)g.tiles_per_frame);
-    const int lt = (int)((u - tl * U) * 64u) + lane;  // the lane's index in the tile (< 1024)
+    const int lt = (int)((u - tile * U) * 64u) + lane;  // the lane's index in the tile (< 1024)
     const bool active = lt < g.k * g.cpr;
     const uint32_t q = __umul24((uint32_t)lt, g.cpr_inv) >> 20;  // lt / cpr
     const int col = active ? lt - (int)__umul24(q, (uint32_t)g.cpr) : 0;
@@ -740,22 +776,21 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
       ex.EN = ex.SX02 = ex.SX13 = ex.SY02 = ex.SY13 = 0;
       ex.rounds = 0;
     };
-    // 12 per-lane values summed over the wave into the frame's sums: device
-    // atomics (fire and forget: no wave waits for another); fused step: the
-    // workgroup's totals in LDS
+    // 12 per-lane values summed over the wave into the frame's sums (fused
+    // step: its accumulator): device atomics (fire and forget: no wave waits
+    // for another)
     auto emit = [&](uint32_t (&v)[12]) {
       wave_sums12(v);
       // lane 16 r + 15 holds values 3 r .. 3 r + 2: range r's N, sum x, sum y
       const int rr = lane >> 4;
       if ((lane & 15) == 15 && rr < NR) {
         unsigned long long* dst =
-            reinterpret_cast<unsigned long long*>(&a.sums[(int64_t)f * a.sums_ranges + a.range_offset + rr].points);
+            a.fused ? a.frame_acc + 16 * (int64_t)f + 3 * rr
+                    : reinterpret_cast<unsigned long long*>(
+                          &a.sums[(int64_t)f * a.sums_ranges + a.range_offset + rr].points);
 #pragma unroll
         for (int j = 0; j < 3; ++j)
-          if (v[j]) {
-            atomicAdd(dst + j, (unsigned long long)v[j]);
-            if (a.fused) lds_add_u64(kLdsTotals + 8u * (uint32_t)(3 * rr + j), v[j]);
-          }
+          if (v[j]) atomicAdd(dst + j, (unsigned long long)v[j]);
       }
     };
     // One drain round: lanes 0..take-1 take the last take records, resolve
@@ -1008,8 +1043,18 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
                         __umul24((uint32_t)half, nb2);
     }
     unpack_exc(acc);
+    if (a.fused) {
+      examine();
+      count_done();
+    }
     emit(acc);
-    u = __builtin_amdgcn_readfirstlane(next) + (blockDim.x >> 6);  // after the waves' first units
+    if (a.fused) pend_f = f;
+    u = u_begin + __builtin_amdgcn_readfirstlane(next) + (blockDim.x >> 6);  // after the waves' first units
+  }
+  if (a.fused) {  // this wave's last counts
+    examine();
+    count_done();
+    examine();
   }
   // the exact-path word count: per workgroup in LDS, one device atomic by its
   // last wave (AUTO's measured share, ChromaTables::flagged_words)
@@ -1022,25 +1067,12 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     }
   }
   if (!a.fused) return;
-  // every wave's sums atomics performed at L2 before the workgroup reads them
-  // back (with L2 loads: this CU's L1 never saw them)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // fused step: the targets of this workgroup's frames, from their sums
-  if (a.targets) {
-    for (int64_t i = t; i < (f_end - f_first) * NR; i += blockDim.x) {
-      const int64_t o = (f_first + i / NR) * a.sums_ranges + a.range_offset + i % NR;
-      unsigned long long* sp = reinterpret_cast<unsigned long long*>(&a.sums[o].points);
-      const uint64_t n = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t sx = __hip_atomic_load(sp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t sy = __hip_atomic_load(sp + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      a.targets[o] = target_of(n, sx, sy, a.width, a.height);
-    }
-  }
-  // fused step: the per-target totals.  Every workgroup stores its totals; the
+  // fused step: the per-target totals (the workgroup's finalized frames'
+  // sums, in LDS once every wave is here).  Every workgroup stores its totals; the
   // last one to finish (a device-scope counter, reset by it for the next
   // launch) sums them into a.totals.
   if (!a.totals) return;
+  __syncthreads();
   // wave 0 alone publishes (its 12 stores, one device-scope fence: an L2
   // write-back per workgroup, not per wave) and counts the workgroup done
   if (t < 64) {
@@ -1291,18 +1323,20 @@ bool chroma_geometry_ok(const KernelArgs& a) {
   return chroma_geometry(a, g);
 }
 
-// The fused step hands each workgroup (one per CU) whole frames: at least 4
-// per workgroup keeps the imbalance of n_frames / CUs to a quarter frame.
+// The fused step splits the units evenly over the workgroups and completes
+// frames by their unit counts: any batch the kernel takes (not the
+// verification mode, which writes masks instead).
 bool chroma_fused_ok(const KernelArgs& a) {
   ChromaGeom g;
-  return !a.masks && chroma_geometry(a, g) && (int64_t)a.n_frames >= 4 * (int64_t)device_cus();
+  return !a.masks && chroma_geometry(a, g);
 }
 
 int launch_chroma(const KernelArgs& a, const ChromaTables* ct, bool write_masks, hipStream_t s) {
   ChromaGeom g;
   if (!chroma_geometry(a, g)) return hipErrorNotSupported;
   if (g.n_tiles == 0) return hipSuccess;
-  if (a.fused && (write_masks || !chroma_fused_ok(a) || !a.wg_part || !a.wg_cnt)) return hipErrorInvalidValue;
+  if (a.fused && (write_masks || !chroma_fused_ok(a) || !a.wg_part || !a.wg_cnt || !a.frame_acc || !a.frame_done))
+    return hipErrorInvalidValue;
   if (a.layout == TRIK_HSV_LAYOUT_YUYV)
     return write_masks ? launch_nr<TRIK_HSV_LAYOUT_YUYV, true>(a, g, ct, s)
                        : launch_nr<TRIK_HSV_LAYOUT_YUYV, false>(a, g, ct, s);

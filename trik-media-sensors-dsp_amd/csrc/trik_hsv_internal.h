@@ -141,16 +141,20 @@ struct KernelArgs {
   const unsigned long long* gate = nullptr;
   unsigned long long gate_max = 0;
   int32_t gate_le = 0;
-  // The fused step (chroma-run kernel; chroma_fused_ok): whole frames per
-  // workgroup, so a frame's sums are zeroed, added and read back inside one
-  // workgroup (no memset launch); the same launch writes the targets and the
-  // per-target batch totals (the last workgroup sums the workgroups' partial
-  // totals).  DESIGN.md section 4.5.
+  // The fused step (chroma-run kernel; chroma_fused_ok): the workgroups split
+  // the batch's wave-sized units evenly, whatever the frame boundaries; a
+  // frame's units add into its accumulator (frame_acc, 128 B per frame) and
+  // count themselves done (frame_done); the wave that counts a frame's last
+  // unit reads and clears the accumulator, stores the frame's sums and
+  // targets and adds them to its workgroup's totals; the last workgroup sums
+  // the workgroups' partial totals.  One launch, no memset.  DESIGN.md 4.5.
   int32_t fused = 0;
   TrikHsvTarget* targets = nullptr;       // [n_frames][sums_ranges], or NULL
   TrikHsvTargetSums* totals = nullptr;    // [sums_ranges], or NULL
   unsigned long long* wg_part = nullptr;  // scratch: [workgroups][12]
   uint32_t* wg_cnt = nullptr;             // scratch: 0 between launches
+  unsigned long long* frame_acc = nullptr;  // scratch: [n_frames][16], 0 between launches
+  uint32_t* frame_done = nullptr;           // scratch: [n_frames], 0 between launches
 };
 
 // The target of one (frame, range) from its sums: WSEQ:486-505 (unsigned

@@ -522,6 +522,11 @@ static int launch_rows2(const PreviewArgs& a, hipStream_t s) {
   if (a.rows2_first < 0 || (!yuyv && a.layout != TRIK_HSV_LAYOUT_OV7670) || a.out_w % px || a.out_ll != 2 * a.out_w ||
       (!a.meta && !a.tables))
     return hipErrorNotSupported;
+  // every unit loads source pixels 2c .. 2c + 1 of each of its output columns
+  // c < out_w, written or not (WIN masks the unwritten ones after the load):
+  // they must lie in the row, or the last row of the last frame reads past
+  // the buffer (e.g. a 480-wide frame under a 320-wide preview)
+  if (2LL * a.out_w > a.width) return hipErrorNotSupported;
   const auto al = [](int64_t v, int64_t m) { return v % m == 0; };
   if (!al((int64_t)reinterpret_cast<uintptr_t>(a.frames), 16) || !al(a.line_length, 16) ||
       (a.n_frames > 1 && !al(a.frame_stride, 16)) || !al((int64_t)reinterpret_cast<uintptr_t>(a.previews), 8) ||
