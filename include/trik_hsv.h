@@ -498,10 +498,10 @@ int32_t trik_hsv_batch_sums(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvFra
 /* Hot-kernel selection of one handle for its trik_hsv_batch_sums /
  * _process_batch / _masks / _blob_batch calls and process() (tests and A/B
  * runs; other handles are not affected).  TRIK_HSV_HOT_AUTO (the default)
- * picks the chroma-run kernel for batches of at least
- * TRIK_HSV_CHROMA_MIN_PIXELS pixels whose geometry it takes and whose range
- * set sends at most TRIK_HSV_CHROMA_MAX_SHARE of the words to its exact path
- * (see trik_hsv_chroma_share), the stripe kernel otherwise -- always for a
+ * picks, per group of 4 ranges, the chroma-run kernel for batches of at
+ * least TRIK_HSV_CHROMA_MIN_PIXELS pixels whose geometry it takes when the
+ * group's tables send at most TRIK_HSV_CHROMA_MAX_SHARE of the words to its
+ * exact path (see trik_hsv_chroma_share), the stripe kernel otherwise -- always for a
  * group of ranges that accepts every hue and saturation (value bands), which
  * the stripe kernel tests by value alone; all kernels give the same results.
  * The first batch with a new range set is not held up by that

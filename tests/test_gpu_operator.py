@@ -161,7 +161,7 @@ def test_batch_auto_range_large_batch(hsv, oracle_mod, layout):
     # square frames: 2:1 maps whose written columns end before out_w (the row
     # kernel would load past the row; the gather takes them)
     (480, 480, 960, 320, 240, 640, LAYOUT_YUYV, 1),
-    (240, 240, 240, 160, 120, 320, LAYOUT_OV7670, 1),
+    (256, 256, 256, 160, 128, 320, LAYOUT_OV7670, 1),
 ])
 def test_batch_preview(hsv, oracle_mod, w, h, ll, ow, oh, oll, layout, kind):
     import torch

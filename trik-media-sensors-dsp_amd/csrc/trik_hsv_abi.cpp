@@ -300,6 +300,12 @@ struct TableSet {
     }
     return chroma_share;
   }
+  // group g's own expected share (AUTO plans each group by its own tables),
+  // or -1 while the builder's readback is in flight
+  double group_share(int g) {
+    if (!chroma_built || share() < 0) return -1.0;
+    return (double)h_cost[g] / 4294967296.0;
+  }
 };
 constexpr int kTableSets = 4;
 
@@ -363,8 +369,7 @@ struct TrikCvHandle {
   // zero between launches), shared by this handle's calls
   unsigned long long* d_wg_part = nullptr;
   uint32_t* d_wg_cnt = nullptr;
-  unsigned long long* d_frame_acc = nullptr;
-  uint32_t* d_frame_done = nullptr;
+  unsigned long long* d_frame_acc = nullptr;  // [frames][16]: 12 sums, the unit count
   int64_t frame_acc_cap = 0;  // frames
   StreamUses fused_users;
 
@@ -427,7 +432,7 @@ void free_resources(TrikCvHandle* h) {
   h->d_blob_top = nullptr; h->d_blob_top_cap = 0;
   h->d_blob_targets = nullptr; h->d_blob_targets_cap = 0;
   h->d_wg_part = nullptr; h->d_wg_cnt = nullptr;
-  h->d_frame_acc = nullptr; h->d_frame_done = nullptr; h->frame_acc_cap = 0;
+  h->d_frame_acc = nullptr; h->frame_acc_cap = 0;
   h->sums_set = h->pending_set = nullptr;
   h->alg_ready = false;
 }
@@ -648,7 +653,7 @@ HotPlan plan_hot(TrikCvHandle* h, TableSet& t, int g, int groups, bool big, bool
   *rc = ensure_chroma(t, groups, s);
   if (*rc) return kPlanStripe;
   if (choice == TRIK_HSV_HOT_CHROMA) return kPlanChroma;
-  const double sh = t.share();
+  const double sh = t.group_share(g);
   if (sh < 0) return kPlanGated;  // the share is still in flight: no host wait
   if (sh > TRIK_HSV_CHROMA_MAX_SHARE) return kPlanStripe;
   // the input's own share, measured on earlier batches: input that
@@ -705,8 +710,8 @@ int32_t note_uses(TrikCvHandle* h, TableSet* set, bool maps, hipStream_t s, Stre
 }
 
 // The fused step's scratch, allocated on first use: one slot of 12 totals per
-// CU and the last-workgroup counter; per frame a 128-byte accumulator (its
-// own cache line) and a unit-done count.  All zeroed once; every launch leaves
+// CU and the last-workgroup counter; per frame a 128-byte line holding its 12
+// accumulators and its unit-done count.  All zeroed once; every launch leaves
 // them zero.  A larger batch reallocates the per-frame part (after the
 // launches still using it: the caller ordered s after them).
 int32_t ensure_fused_scratch(TrikCvHandle* h, int64_t n_frames, hipStream_t s) {
@@ -726,12 +731,11 @@ int32_t ensure_fused_scratch(TrikCvHandle* h, int64_t n_frames, hipStream_t s) {
       h->frame_acc_cap = 0;
     }
     const int64_t cap = n_frames < 1024 ? 1024 : n_frames;
-    const size_t bytes = (size_t)cap * (128 + 4);
+    const size_t bytes = (size_t)cap * 128;
     void* p = nullptr;
     HIP_TRY(hipMalloc(&p, bytes));
     HIP_TRY(hipMemsetAsync(p, 0, bytes, s));
     h->d_frame_acc = static_cast<unsigned long long*>(p);
-    h->d_frame_done = reinterpret_cast<uint32_t*>(h->d_frame_acc + 16 * cap);
     h->frame_acc_cap = cap;
   }
   return 0;
@@ -809,7 +813,6 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
         a.wg_part = h->d_wg_part;
         a.wg_cnt = h->d_wg_cnt;
         a.frame_acc = h->d_frame_acc;
-        a.frame_done = h->d_frame_done;
       }
       e = launch_chroma(a, t->d_chroma + g, masks != nullptr, s);
       if (e == hipSuccess) {

@@ -709,7 +709,8 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         lds_add_u64(kLdsTotals + 24u * (uint32_t)lane + 16u, sy);
       }
     }
-    if (lane == 0) __hip_atomic_store(a.frame_done + F, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0)  // the unit count (word 24 of the frame's line)
+      __hip_atomic_store(reinterpret_cast<uint32_t*>(acc + 12), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   auto examine = [&]() {  // the count issued at the previous unit end
     if (chk_f < 0) return;
@@ -720,7 +721,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
     if (pend_f < 0) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t r = 0;
-    if (lane == 0) r = atomicAdd(a.frame_done + pend_f, 1u);
+    if (lane == 0) r = atomicAdd(reinterpret_cast<uint32_t*>(a.frame_acc + 16 * (int64_t)pend_f + 12), 1u);
     chk_r = r;
     chk_f = pend_f;
     pend_f = -1;
@@ -1178,63 +1179,101 @@ __global__ __launch_bounds__(kMaxBlock) void blob_chroma_meta_kernel(BlobArgs a,
     }
     qn = rest;
   };
-  for (uint32_t base = blockIdx.x * (uint32_t)kMaxBlock; base < g.total; base += gridDim.x * (uint32_t)kMaxBlock) {
-    const uint32_t item = base + (uint32_t)t;
-    const bool valid = item < g.total;
-    const uint64_t vm = __builtin_amdgcn_ballot_w64(valid);
-    const uint32_t it = valid ? item : 0u;
-    const uint32_t f = fdiv(it, g.per_frame), rem = it - f * g.per_frame.d;
-    const uint32_t mr = fdiv(rem, g.per_row), ch = rem - mr * g.per_row.d;
-    const uint8_t* p = a.frames + (int64_t)f * a.frame_stride + (int64_t)(4 * mr) * ll + 16 * (int64_t)ch;
+  // Items in grid-stride order; a lane's item is four pixel rows of its 16
+  // columns.  The rows are software-pipelined across items: the next row
+  // (the next item's first at an item's last) is loaded while this one is
+  // processed, two 32-byte buffers per lane (the loads past the batch re-read
+  // the lane's last item: unconditional, so waits stay "this row's data").
+  const uint32_t stride = gridDim.x * (uint32_t)kMaxBlock;
+  uint32_t base = blockIdx.x * (uint32_t)kMaxBlock;
+  if (base >= g.total) return;
+  struct Item {
+    const uint8_t* p;
+    uint32_t f, mr, ch;
+    bool valid;
+  };
+  auto item_at = [&](uint32_t b, const Item& fallback) {
+    Item r;
+    const uint32_t item = b + (uint32_t)t;
+    r.valid = item < g.total;
+    if (!r.valid && b != blockIdx.x * (uint32_t)kMaxBlock) return Item{fallback.p, fallback.f, fallback.mr, fallback.ch, false};
+    const uint32_t it = r.valid ? item : 0u;
+    r.f = fdiv(it, g.per_frame);
+    const uint32_t rem = it - r.f * g.per_frame.d;
+    r.mr = fdiv(rem, g.per_row);
+    r.ch = rem - r.mr * g.per_row.d;
+    r.p = a.frames + (int64_t)r.f * a.frame_stride + (int64_t)(4 * r.mr) * ll + 16 * (int64_t)r.ch;
+    return r;
+  };
+  Item cur = item_at(base, Item{a.frames, 0u, 0u, 0u, false});
+  uint4 by[2], bc[2];
+  by[0] = *reinterpret_cast<const uint4*>(cur.p);
+  bc[0] = *reinterpret_cast<const uint4*>(cur.p + plane);
+  for (;;) {
+    const uint64_t vm = __builtin_amdgcn_ballot_w64(cur.valid);
+    const uint32_t nb = base + stride;
+    const Item nxt = item_at(nb < g.total ? nb : base, cur);
     uint32_t cnt[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const uint4 vy = *reinterpret_cast<const uint4*>(p + r * ll);
-      const uint4 vc = *reinterpret_cast<const uint4*>(p + r * ll + plane);
+      // the next row: this item's r + 1, or the next item's row 0
+      const uint8_t* np = r < 3 ? cur.p + (r + 1) * ll : nxt.p;
+      by[(r + 1) & 1] = *reinterpret_cast<const uint4*>(np);
+      bc[(r + 1) & 1] = *reinterpret_cast<const uint4*>(np + plane);
+      const uint4 vy = by[r & 1], vc = bc[r & 1];
       const uint32_t yy[4] = {vy.x, vy.y, vy.z, vy.w}, cc[4] = {vc.x, vc.y, vc.z, vc.w};
-      uint32_t w[8], d[8], cut[8];
-      u32x2 mm[8];
+      // the row's 8 words in two halves of 4 (registers: the next row's
+      // buffer stays live)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) stripe_px::ov7670_words(yy[k], cc[k], w[2 * k], w[2 * k + 1]);
+      for (int hf = 0; hf < 2; ++hf) {
+        uint32_t w[4], d[4], cut[4];
+        u32x2 mm[4];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint32_t c = chroma_of(w[i]);
-        d[i] = ld16(kLdsRuns + 2u * c);
-        cut[i] = ld16(kLdsBlocks + ((c >> 3) & 0x1FFEu));
-      }
+        for (int k = 0; k < 2; ++k) stripe_px::ov7670_words(yy[2 * hf + k], cc[2 * hf + k], w[2 * k], w[2 * k + 1]);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) mm[i] = ld64(kLdsPairs + (cut[i] & 0xFFu));
-#pragma unroll
-      for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(d[i]), "+v"(cut[i]));
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        uint32_t e0, e1;
-        uint64_t q0, q1;
-        select2(w[i], d[i], cut[i], mm[i].x, mm[i].y, vm, e0, e1, q0, q1);
-        cnt[i >> 1] += e0 + e1;  // one range: the spread masks are 0 or 1
-        const uint64_t bal = q0 | q1;
-        if (bal == 0) continue;  // no lane of the wave flagged this word slot (the common case)
-        const uint32_t idx =
-            __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-        if (__builtin_amdgcn_inverse_ballot_w64(bal)) {
-          const uint32_t qa = __builtin_amdgcn_readfirstlane(qbase_s + 8u * (uint32_t)qn) + 8u * idx;
-          *(lds32_t)(uintptr_t)qa = w[i];
-          *(lds32_t)(uintptr_t)(qa + 4u) = (uint32_t)lane | ((uint32_t)(i >> 1) << 6);
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t c = chroma_of(w[i]);
+          d[i] = ld16(kLdsRuns + 2u * c);
+          cut[i] = ld16(kLdsBlocks + ((c >> 3) & 0x1FFEu));
         }
-        qn += __builtin_popcountll(bal);
-        if (qn >= 64) drain(64);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mm[i] = ld64(kLdsPairs + (cut[i] & 0xFFu));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(d[i]), "+v"(cut[i]));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int wi = 4 * hf + i;  // the word's index in the row: metapixel wi >> 1
+          uint32_t e0, e1;
+          uint64_t q0, q1;
+          select2(w[i], d[i], cut[i], mm[i].x, mm[i].y, vm, e0, e1, q0, q1);
+          cnt[wi >> 1] += e0 + e1;  // one range: the spread masks are 0 or 1
+          const uint64_t bal = q0 | q1;
+          if (bal == 0) continue;  // no lane of the wave flagged this word slot (the common case)
+          const uint32_t idx =
+              __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+          if (__builtin_amdgcn_inverse_ballot_w64(bal)) {
+            const uint32_t qa = __builtin_amdgcn_readfirstlane(qbase_s + 8u * (uint32_t)qn) + 8u * idx;
+            *(lds32_t)(uintptr_t)qa = w[i];
+            *(lds32_t)(uintptr_t)(qa + 4u) = (uint32_t)lane | ((uint32_t)(wi >> 1) << 6);
+          }
+          qn += __builtin_popcountll(bal);
+          if (qn >= 64) drain(64);
+        }
       }
     }
     while (qn > 0) drain(qn < 64 ? qn : 64);
     __builtin_amdgcn_wave_barrier();
     const uint32_t extra = *(lds32_t)(uintptr_t)my_counts;
     *(lds32_t)(uintptr_t)my_counts = 0u;
-    if (valid) {
+    if (cur.valid) {
       uint32_t flags = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) flags |= (cnt[j] + ((extra >> (8 * j)) & 0xFFu) > 2u ? 1u : 0u) << (8 * j);
-      *reinterpret_cast<uint32_t*>(a.meta + ((int64_t)f * g.bh + mr) * g.bw + 4 * (int64_t)ch) = flags;
+      *reinterpret_cast<uint32_t*>(a.meta + ((int64_t)cur.f * g.bh + cur.mr) * g.bw + 4 * (int64_t)cur.ch) = flags;
     }
+    if (nb >= g.total) break;
+    base = nb;
+    cur = nxt;
   }
 }
 
@@ -1335,7 +1374,7 @@ int launch_chroma(const KernelArgs& a, const ChromaTables* ct, bool write_masks,
   ChromaGeom g;
   if (!chroma_geometry(a, g)) return hipErrorNotSupported;
   if (g.n_tiles == 0) return hipSuccess;
-  if (a.fused && (write_masks || !chroma_fused_ok(a) || !a.wg_part || !a.wg_cnt || !a.frame_acc || !a.frame_done))
+  if (a.fused && (write_masks || !chroma_fused_ok(a) || !a.wg_part || !a.wg_cnt || !a.frame_acc))
     return hipErrorInvalidValue;
   if (a.layout == TRIK_HSV_LAYOUT_YUYV)
     return write_masks ? launch_nr<TRIK_HSV_LAYOUT_YUYV, true>(a, g, ct, s)

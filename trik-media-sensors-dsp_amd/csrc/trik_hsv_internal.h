@@ -143,8 +143,9 @@ struct KernelArgs {
   int32_t gate_le = 0;
   // The fused step (chroma-run kernel; chroma_fused_ok): the workgroups split
   // the batch's wave-sized units evenly, whatever the frame boundaries; a
-  // frame's units add into its accumulator (frame_acc, 128 B per frame) and
-  // count themselves done (frame_done); the wave that counts a frame's last
+  // frame's units add into its accumulator (frame_acc: one 128-B line per
+  // frame, 12 sums and the unit count) and count themselves done; the wave
+  // that counts a frame's last
   // unit reads and clears the accumulator, stores the frame's sums and
   // targets and adds them to its workgroup's totals; the last workgroup sums
   // the workgroups' partial totals.  One launch, no memset.  DESIGN.md 4.5.
@@ -154,7 +155,6 @@ struct KernelArgs {
   unsigned long long* wg_part = nullptr;  // scratch: [workgroups][12]
   uint32_t* wg_cnt = nullptr;             // scratch: 0 between launches
   unsigned long long* frame_acc = nullptr;  // scratch: [n_frames][16], 0 between launches
-  uint32_t* frame_done = nullptr;           // scratch: [n_frames], 0 between launches
 };
 
 // The target of one (frame, range) from its sums: WSEQ:486-505 (unsigned
