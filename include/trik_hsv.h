@@ -478,11 +478,10 @@ int32_t trik_hsv_process_batch(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsv
 
 /* The full batched step: as trik_hsv_process_batch, plus the per-target
  * batch totals (totals_dev[r] = the sum over the frames of sums_dev[f][r], as
- * trik_hsv_batch_totals).  Where the chroma-run kernel runs on a batch that
- * gives every CU at least 4 whole frames, each group of <= 4 ranges is ONE
- * launch: the kernel zeroes its frames' sums, adds them, and writes the
- * targets and the totals itself; otherwise the same outputs come from the
- * separate kernels.
+ * trik_hsv_batch_totals).  Where the chroma-run kernel runs, each group of
+ * <= 4 ranges is ONE launch: the kernel writes every frame's sums and targets
+ * as the frame completes and the totals at its end (scratch held by the
+ * handle); otherwise the same outputs come from the separate kernels.
  * totals_dev: [n_ranges] TrikHsvTargetSums (device, not NULL). */
 int32_t trik_hsv_process_batch_totals(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvFrameBatch* batch,
                                       const TRIK_VIDTRANSCODE_CV_InArgsAlg* ranges, int32_t n_ranges,

@@ -23,7 +23,8 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "trik-media-sensors-dsp_amd"))
+# TRIK_HSV_PKG_DIR: a directory holding another build's trik_hsv package (A/B)
+sys.path.insert(0, os.environ.get("TRIK_HSV_PKG_DIR", os.path.join(ROOT, "trik-media-sensors-dsp_amd")))
 HBM_PEAK_GBS = 8000.0
 
 

@@ -1,12 +1,14 @@
 """The fused full step (trik_hsv_process_batch_totals): the chroma-run kernel
-stores each frame's sums, writes its targets and the per-target batch totals
-in the same launch when every CU gets at least 4 whole frames
-(trik_hsv_chroma.hip: chroma_fused_ok).
+splits the batch's units evenly over its workgroups, and the wave that counts
+a frame's last unit stores the frame's sums and targets; the last workgroup
+writes the per-target batch totals -- one launch (trik_hsv_chroma.hip:
+chroma_kernel, chroma_fused_ok).
 
 Held to the separate-kernel path (the hot kernel adding into zeroed sums,
 then the epilogue and totals kernels) bit for bit, and to the oracle
 (oracle/trik_oracle.c: WSEQ:251-354 and the epilogue WSEQ:486-505) on sampled
-frames.  Batch sizes straddle the fused rule (4 frames per CU).
+frames.  Batch sizes that do not divide over the workgroups put a frame's
+units in two workgroups (1100, 1000, 257, 40 frames).
 """
 
 import numpy as np
@@ -66,7 +68,7 @@ def _fused(torch, hsv, det, frames, n, ranges):
     return sums, targets, totals
 
 
-@pytest.mark.parametrize("n,kind", [(1024, 0), (1024, 1), (1100, 0), (1000, 0), (2048, 1)])
+@pytest.mark.parametrize("n,kind", [(1024, 0), (1024, 1), (1100, 0), (1000, 0), (2048, 1), (257, 1), (40, 0)])
 def test_fused_step_equals_separate_kernels(torch_dev, hsv, oracle_mod, n, kind):
     torch = torch_dev
     frames = _frames(torch, hsv, n, kind)

@@ -247,6 +247,47 @@ __device__ __forceinline__ void stage_exact_tables(const RangeTables* t, int tid
   }
 }
 
+// The hot kernels' LDS image (block words, mask-pair palette, run
+// descriptors, exact-path tables) staged by a 1024-lane workgroup: every
+// lane issues all its global loads (8 run chunks, a block chunk, a palette
+// entry, the exact tables' entries) before its first LDS store, so the
+// workgroup pays one load latency instead of one per chunk (a load-store
+// loop waited ~8 times).
+__device__ __forceinline__ void stage_chroma_image(const ChromaTables* ct, const RangeTables* rt, int t) {
+  constexpr int kRunChunks = 131072 / 16, kBlockChunks = 8192 / 16;
+  static_assert(kRunChunks % 1024 == 0 && kBlockChunks <= 1024 && kChromaPalette <= 1024, "1024-lane staging");
+  const u32x4* runs = reinterpret_cast<const u32x4*>(ct->runs);
+  u32x4 r[kRunChunks / 1024];
+#pragma unroll
+  for (int k = 0; k < kRunChunks / 1024; ++k) r[k] = runs[t + 1024 * k];
+  u32x4 blk = {0u, 0u, 0u, 0u};
+  if (t < kBlockChunks) blk = reinterpret_cast<const u32x4*>(ct->blocks)[t];
+  uint32_t p0 = 0, p1 = 0;
+  if (t < kChromaPalette) {
+    p0 = ct->palette[2 * t];
+    p1 = ct->palette[2 * t + 1];
+  }
+  uint32_t l43 = 0, l255 = 0, hu = 0, sm = 0, vm = 0;
+  if (t < 256) {
+    l43 = rt->lut43[t];
+    l255 = rt->lut255[t];
+    hu = rt->hue[t];
+    sm = rt->smask[t];
+    vm = rt->vmask[t];
+  }
+#pragma unroll
+  for (int k = 0; k < kRunChunks / 1024; ++k) *(lds128_t)(uintptr_t)(kLdsRuns + 16u * (uint32_t)(t + 1024 * k)) = r[k];
+  if (t < kBlockChunks) *(lds128_t)(uintptr_t)(kLdsBlocks + 16u * (uint32_t)t) = blk;
+  if (t < kChromaPalette) st64(kLdsPairs + 8u * (uint32_t)t, p0, p1);
+  if (t < 256) {
+    *(lds16_t)(uintptr_t)(kLdsLut43 + 2 * t) = (uint16_t)l43;
+    *(lds16_t)(uintptr_t)(kLdsLut255 + 2 * t) = (uint16_t)l255;
+    *(lds8_t)(uintptr_t)(kLdsHue + t) = (uint8_t)hu;
+    *(lds8_t)(uintptr_t)(kLdsSat + t) = (uint8_t)sm;
+    *(lds8_t)(uintptr_t)(kLdsVal + t) = (uint8_t)vm;
+  }
+}
+
 // One workgroup of 1024 per V: the exact T-bit mask of every (Y, U) -- the
 // 256 chromas' profiles, two Y per YUYV word through exact_mask (the stripe
 // kernel's arithmetic on LDS tables, held to the oracle on all 2^24 triples)
@@ -637,20 +678,8 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
   if (gated_out(a.gate, a.gate_max, a.gate_le)) return;
   constexpr int CW = kChunkWords;
   const int t = threadIdx.x;
-  {  // stage the block words, the mask-pair table, the run descriptors and the exact-path tables
-    for (int i = t; i < 8192 / 16; i += blockDim.x)
-      *(lds128_t)(uintptr_t)(kLdsBlocks + 16 * i) = reinterpret_cast<const u32x4*>(ct->blocks)[i];
-    for (int i = t; i < kChromaPalette; i += blockDim.x) st64(kLdsPairs + 8 * i, ct->palette[2 * i], ct->palette[2 * i + 1]);
-    for (int i = t; i < 131072 / 16; i += blockDim.x)
-      *(lds128_t)(uintptr_t)(kLdsRuns + 16 * i) = reinterpret_cast<const u32x4*>(ct->runs)[i];
-    for (int i = t; i < 256; i += blockDim.x) {
-      *(lds16_t)(uintptr_t)(kLdsLut43 + 2 * i) = a.tables->lut43[i];
-      *(lds16_t)(uintptr_t)(kLdsLut255 + 2 * i) = a.tables->lut255[i];
-      *(lds8_t)(uintptr_t)(kLdsHue + i) = a.tables->hue[i];
-      *(lds8_t)(uintptr_t)(kLdsSat + i) = a.tables->smask[i];
-      *(lds8_t)(uintptr_t)(kLdsVal + i) = a.tables->vmask[i];
-    }
-  }
+  static_assert(64 * kHotWaves == 1024, "the hot kernel's workgroup stages the image");
+  stage_chroma_image(ct, a.tables, t);  // the block words, palette, run descriptors, exact-path tables
   // This workgroup's units: an even share of the batch's wave-sized units
   // (unit u: tile u / U, lanes 64 (u % U) ..), whatever the frame boundaries
   // (a frame's units may lie in several workgroups: the fused step counts
@@ -1131,21 +1160,9 @@ __global__ __launch_bounds__(kMaxBlock) void blob_chroma_meta_kernel(BlobArgs a,
                                                                       const RangeTables* rt) {
   if (gated_out(a.gate, a.gate_max, a.gate_le)) return;
   const int t = threadIdx.x;
-  {  // the chroma kernel's tables (one range), zeroed count words
-    for (int i = t; i < 8192 / 16; i += blockDim.x)
-      *(lds128_t)(uintptr_t)(kLdsBlocks + 16 * i) = reinterpret_cast<const u32x4*>(ct->blocks)[i];
-    for (int i = t; i < kChromaPalette; i += blockDim.x) st64(kLdsPairs + 8 * i, ct->palette[2 * i], ct->palette[2 * i + 1]);
-    for (int i = t; i < 131072 / 16; i += blockDim.x)
-      *(lds128_t)(uintptr_t)(kLdsRuns + 16 * i) = reinterpret_cast<const u32x4*>(ct->runs)[i];
-    for (int i = t; i < 256; i += blockDim.x) {
-      *(lds16_t)(uintptr_t)(kLdsLut43 + 2 * i) = rt->lut43[i];
-      *(lds16_t)(uintptr_t)(kLdsLut255 + 2 * i) = rt->lut255[i];
-      *(lds8_t)(uintptr_t)(kLdsHue + i) = rt->hue[i];
-      *(lds8_t)(uintptr_t)(kLdsSat + i) = rt->smask[i];
-      *(lds8_t)(uintptr_t)(kLdsVal + i) = rt->vmask[i];
-    }
-    *(lds32_t)(uintptr_t)(kLdsBlobCounts + 4u * (uint32_t)t) = 0u;
-  }
+  // the chroma kernel's tables (one range), zeroed count words
+  stage_chroma_image(ct, rt, t);
+  *(lds32_t)(uintptr_t)(kLdsBlobCounts + 4u * (uint32_t)t) = 0u;
   __syncthreads();
   const int lane = t & 63;
   const uint32_t qbase_s = __builtin_amdgcn_readfirstlane(kLdsQueues + (uint32_t)(t >> 6) * (kQueueCap * 8));

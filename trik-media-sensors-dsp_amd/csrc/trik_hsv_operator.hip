@@ -180,9 +180,11 @@ void preview_gather_kernel(PreviewArgs a, PreviewGeom g) {
 // output columns one contiguous window [rows2_c0, rows2_c1) (the line
 // sensor's 5 <= col <= W - 5; zero outside).  Output pixel c' is the odd
 // pixel of source pixel pair c'.  A unit reads 16 bytes per plane and writes
-// its output pixels as 8-byte stores: packed YUYV, 4 words -> 4 pixels (a
-// wave reads 1 KiB of one row); ov7670, 16 luma + 16 chroma bytes -> 8 pixels
-// (U = odd chroma byte, OSEQ:369-373).  No maps, no gather.  Lane t of the
+// its output pixels as 8-byte stores: packed YUYV, 2 x 4 words -> 8 pixels (a
+// wave reads 2 KiB of one row); ov7670, 16 luma + 16 chroma bytes -> 8 pixels
+// (U = odd chroma byte, OSEQ:369-373).  No maps, no gather.  (A YUYV
+// unit is two 16-byte pieces, 8 output pixels: the per-unit address and
+// index work is shared by 8 pixels, as in the ov7670 form.)  Lane t of the
 // grid takes units t, t + T, t + 2T, ... (T = the grid's lanes), kRowsQ of
 // them per round with their loads issued together; the (frame, row, group) of
 // the next unit follows from the current one by adding T's decomposition with
@@ -197,7 +199,7 @@ struct PreviewRowsGeom {
   uint32_t total;
   uint32_t step_f, step_r, step_q;  // the grid's lane count T as (frames, rows, groups)
 };
-constexpr int kRowsQ = 2;  // units per lane and round
+constexpr int kRowsQ = 1;  // units per lane and round (8 output pixels: 2 spill at 64 VGPRs)
 constexpr uint32_t rgb565x(uint32_t rgb) {  // write_px565's value
   return ((rgb >> 19) & 0x001fu) | ((rgb >> 5) & 0x07e0u) | ((rgb << 8) & 0xf800u);
 }
@@ -207,7 +209,7 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
   using namespace stripe_px;
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   constexpr bool YUYV = LAYOUT == TRIK_HSV_LAYOUT_YUYV;
-  constexpr int PX = YUYV ? 4 : 8;  // output pixels per unit
+  constexpr int PX = 8;  // output pixels per unit
   if (!a.meta) {
     const u32x4* src = reinterpret_cast<const u32x4*>(a.tables);
     typedef __attribute__((address_space(3))) u32x4* lds_u128_wptr;
@@ -250,9 +252,10 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
         tsx[u] = ts[2];
       }
       const uint8_t* src = a.frames + (int64_t)fl * a.frame_stride +
-                           (int64_t)((uint32_t)a.rows2_first + 2u * r) * a.line_length + 16 * (int64_t)q;
+                           (int64_t)((uint32_t)a.rows2_first + 2u * r) * a.line_length + (YUYV ? 32 : 16) * (int64_t)q;
       w[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
-      if (!YUYV) wc[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + plane));
+      // YUYV: the unit's second piece; ov7670: its chroma bytes
+      wc[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(YUYV ? src + 16 : src + plane));
       advance();
     }
 #pragma unroll
@@ -260,6 +263,7 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
       uint32_t ws[PX];
       if (YUYV) {
         ws[0] = w[u].x; ws[1] = w[u].y; ws[2] = w[u].z; ws[3] = w[u].w;
+        ws[4] = wc[u].x; ws[5] = wc[u].y; ws[6] = wc[u].z; ws[7] = wc[u].w;
       } else {  // the word (-, U, Y1, V) of output pixel 2d + j: luma byte 2j + 1, chroma bytes 2j, 2j + 1
         const uint32_t yy[4] = {w[u].x, w[u].y, w[u].z, w[u].w}, cc[4] = {wc[u].x, wc[u].y, wc[u].z, wc[u].w};
 #pragma unroll
@@ -518,7 +522,7 @@ __global__ __launch_bounds__(kBlock) void auto_range_kernel(AutoRangeArgs a) {
 // preview_rows2_kernel); hipErrorNotSupported otherwise.
 static int launch_rows2(const PreviewArgs& a, hipStream_t s) {
   const bool yuyv = a.layout == TRIK_HSV_LAYOUT_YUYV;
-  const int px = yuyv ? 4 : 8;
+  const int px = 8;  // output pixels per unit
   if (a.rows2_first < 0 || (!yuyv && a.layout != TRIK_HSV_LAYOUT_OV7670) || a.out_w % px || a.out_ll != 2 * a.out_w ||
       (!a.meta && !a.tables))
     return hipErrorNotSupported;
