@@ -317,7 +317,7 @@ def main():
     # scene frames: camera-like content, the same step.
     # Last before the warmup, back to back: the timed steps then start from
     # the clocks of a running workload, not from the power controller's
-    # transient after the idle gaps above (profiles/r04a_driver_cmd_launches.txt:
+    # transient after the idle gaps above (profiles/r04/r04a_driver_cmd_launches.txt:
     # the same launch ran 478-700 us across those phases)
     scene = None
     if args.scene_launches > 0 and not args.no_extras:

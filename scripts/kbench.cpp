@@ -43,6 +43,7 @@ struct Lib {
   decltype(&trik_hsv_chroma_share) share;
   TRIK_VIDTRANSCODE_CV_Handle h = nullptr;
   std::vector<float> ms;
+  void* (*trace_ptr)() = nullptr;  // timing variants only: the per-wave timestamp trace
 };
 
 template <typename F>
@@ -90,6 +91,7 @@ int main(int argc, char** argv) {
     sym(L.so, "trik_hsv_set_hot_kernel", L.set_hot);
     sym(L.so, "trik_hsv_last_error", L.last_error);
     sym(L.so, "trik_hsv_chroma_share", L.share);
+    L.trace_ptr = reinterpret_cast<void* (*)()>(dlsym(L.so, "trik_trace_ptr"));
     libs.push_back(L);
   }
   if (libs.empty()) return 2;
@@ -181,6 +183,66 @@ int main(int argc, char** argv) {
       printf("%-40s back to back: %.4f ms/step bare, %.4f ms/step with per-launch events, launch %.4f ms, gap %.2f us\n",
              L.path.c_str(), bare / K, with / K, kern / K, 1e3 * (with - kern) / K);
     }
+  }
+  for (Lib& L : libs) {  // per-wave timestamps of one launch in a back-to-back run (trace variants)
+    if (!L.trace_ptr) continue;
+    constexpr int kRec = 6, kMaxWaves = 8192;
+    uint64_t* d_tr = static_cast<uint64_t*>(L.trace_ptr());
+    auto launch = [&]() { (full ? L.step(L.h, &b, all, T, d_sums, d_targets, d_totals, s) : L.sums(L.h, &b, all, T, d_sums, s)); };
+    for (int w = 0; w < 10; ++w) launch();
+    CK(hipMemsetAsync(d_tr, 0, sizeof(uint64_t) * kRec * kMaxWaves, s));
+    launch();
+    launch();  // (the traced launch: the one before it overwrote nothing it reads)
+    CK(hipStreamSynchronize(s));
+    std::vector<uint64_t> tr((size_t)kRec * kMaxWaves);
+    CK(hipMemcpy(tr.data(), d_tr, sizeof(uint64_t) * tr.size(), hipMemcpyDeviceToHost));
+    // records: t0 kernel start, t1 image staged, t2 unit loop left, t3 wave end, units, workgroup
+    std::vector<int> ws;
+    uint64_t t0min = ~0ull, tend = 0;
+    for (int i = 0; i < kMaxWaves; ++i)
+      if (tr[kRec * i]) {
+        ws.push_back(i);
+        t0min = std::min(t0min, tr[kRec * i]);
+        tend = std::max(tend, tr[kRec * i + 3]);
+      }
+    if (ws.empty()) continue;
+    auto us = [&](uint64_t t) { return (t - t0min) / 100.0; };  // s_memrealtime: 100 MHz
+    std::vector<double> st, stg, le, en, un;
+    for (int i : ws) {
+      st.push_back(us(tr[kRec * i]));
+      stg.push_back((tr[kRec * i + 1] - tr[kRec * i]) / 100.0);
+      le.push_back(us(tr[kRec * i + 2]));
+      en.push_back(us(tr[kRec * i + 3]));
+      un.push_back((double)tr[kRec * i + 4]);
+    }
+    auto pct = [](std::vector<double> v, double q) { std::sort(v.begin(), v.end()); return v[(size_t)(q * (v.size() - 1))]; };
+    const double span = us(tend);
+    double idle = 0;
+    for (double x : le) idle += span - x;
+    idle /= (double)ws.size() * span;
+    printf("%-40s trace: %zu waves, span %.1f us; start p50/max %.1f/%.1f; staging p50/max %.1f/%.1f; "
+           "loop end min/p10/p50/p90/max %.1f/%.1f/%.1f/%.1f/%.1f; idle after loop %.1f %%; units/wave min/max %.0f/%.0f\n",
+           L.path.c_str(), ws.size(), span, pct(st, 0.5), pct(st, 1.0), pct(stg, 0.5), pct(stg, 1.0), pct(le, 0.0),
+           pct(le, 0.1), pct(le, 0.5), pct(le, 0.9), pct(le, 1.0), 100 * idle, pct(un, 0.0), pct(un, 1.0));
+    // per workgroup: its first and last wave out of the loop
+    std::vector<double> wfirst(kMaxWaves, 1e30), wlast(kMaxWaves, 0);
+    int nwg = 0;
+    for (int i : ws) {
+      const int g = (int)tr[kRec * i + 5];
+      nwg = std::max(nwg, g + 1);
+      wfirst[g] = std::min(wfirst[g], us(tr[kRec * i + 2]));
+      wlast[g] = std::max(wlast[g], us(tr[kRec * i + 2]));
+    }
+    std::vector<double> spread, lastv;
+    for (int g = 0; g < nwg; ++g)
+      if (wlast[g] > 0) {
+        spread.push_back(wlast[g] - wfirst[g]);
+        lastv.push_back(wlast[g]);
+      }
+    printf("%-40s trace: %d workgroups; in-workgroup loop-end spread p50/p90/max %.1f/%.1f/%.1f us; "
+           "workgroup end min/p50/max %.1f/%.1f/%.1f us\n",
+           L.path.c_str(), nwg, pct(spread, 0.5), pct(spread, 0.9), pct(spread, 1.0), pct(lastv, 0.0), pct(lastv, 0.5),
+           pct(lastv, 1.0));
   }
   const double bytes = (double)fb * frames;
   for (Lib& L : libs) {

@@ -60,7 +60,7 @@ def test_webcam_line_process_vs_oracle(hsv, oracle_mod, geom):
             fr = oracle_mod.wline_scene(w, h, ll, seed, x0=x0 if x0 is None or x0 < w else w // 3, slope=sl)
             out = np.full(oh * oll + 16, 0xCD, np.uint8)
             rc, oa = s.process(fr, (0, 359, 0, 100, vf, vt), out_buffer=out, auto_detect=True)
-            assert rc == 0
+            assert rc == 0, hsv._abi.last_error()
             rrc, ref, ref_pv, _ = oracle_mod.wline_run(fr, w, h, ll, vf, vt, out_width=ow, out_height=oh,
                                                        out_line_length=oll)
             assert rrc == 0
@@ -85,7 +85,7 @@ def test_webcam_line_target_at_the_edges(hsv, oracle_mod, geom):
             fr = oracle_mod.wline_scene(w, h, ll, seed, x0=x0, slope=0.0, line_w=1)
             out = np.full(oh * oll, 0xCD, np.uint8)
             rc, oa = s.process(fr, (0, 359, 0, 100, 0, 30), out_buffer=out)
-            assert rc == 0
+            assert rc == 0, hsv._abi.last_error()
             rrc, ref, ref_pv, _ = oracle_mod.wline_run(fr, w, h, ll, 0, 30, out_width=ow, out_height=oh,
                                                        out_line_length=oll)
             assert rrc == 0 and abs(ref["target_x"]) >= 98  # the target at an edge
@@ -106,7 +106,7 @@ def test_webcam_line_hue_and_sat_ignored(hsv, oracle_mod):
         for hs in ((0, 359, 0, 100), (10, 20, 90, 95), (300, 40, 0, 0)):
             out = np.zeros(120 * 320, np.uint8)
             rc, oa = s.process(fr, hs + (0, 30), out_buffer=out)
-            assert rc == 0
+            assert rc == 0, hsv._abi.last_error()
             outs.append(((oa.alg.targetX, oa.alg.targetY, oa.alg.targetSize), out))
         assert all(o[0] == outs[0][0] and np.array_equal(o[1], outs[0][1]) for o in outs)
     finally:
