@@ -76,9 +76,11 @@ def parse():
     ap.add_argument("--cpu-frames-emul", type=int, default=32,
                     help="sample of the oracle's intrinsic-level emulation (secondary rate)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--event-every", type=int, default=4,
-                    help="bracket every n-th timed step with HIP events for kernel_ms (an event record is a "
-                         "stream packet of a few us: on every step it would inflate ms_per_step)")
+    ap.add_argument("--event-every", type=int, default=0,
+                    help="bracket every n-th timed step with HIP events for kernel_ms; 0 (default): one event "
+                         "pair around the whole timed region when a step is one launch on the stream (the "
+                         "fused step at N = 1), else every 4th step (an event record is a stream packet of a "
+                         "few us: it delays the launch it brackets)")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the cold-batch and scene measurements (PMC passes: only the bench's own launches)")
     ap.add_argument("--hot", choices=["auto", "stripe", "chroma"], default="auto",
@@ -344,23 +346,33 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    every = max(1, args.event_every)
+    # kernel_ms: when a step is exactly one launch on the stream (the fused
+    # step on one rank), one event pair around the timed region: the launches'
+    # average duration, gaps between them included (an upper bound, and no
+    # event packet between launches); otherwise event pairs around every 4th
+    # step's launches
+    single_launch = det.last_hot_kernel() == trik_hsv.HOT_CHROMA and world == 1
+    every = args.event_every if args.event_every > 0 else (0 if single_launch else 4)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(0, args.steps, every)]
+           for _ in range(0, args.steps, every)] if every else []
+    region = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    region[0].record(stream)
     for k in range(args.steps):
-        if k % every == 0:
+        if every and k % every == 0:
             step(*evs[k // every])
         else:
             step()
+    region[1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+    region_ms = region[0].elapsed_time(region[1]) / args.steps
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs) if evs else region_ms
     # what the timed steps reduced: the totals after the last step against a
     # fresh sum of this rank's per-frame sums, reduced the same way
     fresh = batch_totals(sums)
@@ -412,7 +424,10 @@ def main():
                      "traffic": traffic, "traffic_source": traffic_source,
                      "kernel": f"{kname}<YUYV,{T}>", "kernel_ms": round(kern_ms, 4),
                      "kernel_ms_max_rank": round(kern_ms_max, 4),
-                     "kernel_ms_launches": len(evs), "kernel_ms_event_every": every,
+                     "kernel_ms_how": ("one event pair around the timed region / steps (each step is this one "
+                                       "launch)" if not evs else
+                                       f"event pairs around every {every}-th step's launches ({len(evs)} steps)"),
+                     "region_ms_per_step": round(region_ms, 4),
                      "kernel_scope": ("the step's one launch (fused: its frames' sums zeroed and added, targets and totals written "
                                       "by the same kernel)" if fused else
                                       "the step's launches (zero the sums, hot kernel, epilogue, totals)"),

@@ -144,9 +144,8 @@ std::string validate_batch(const TrikHsvFrameBatch* b) {
 // make its stream wait for them (device side) or, before the buffer is
 // rewritten, find out without blocking whether they have finished.
 // One event per stream the handle has enqueued work on, recorded once per
-// call after its last launch (an event record is a packet on the stream that
-// costs the GPU a few microseconds between kernels: one per call, not one per
-// buffer).  A new stream takes over the event of one whose recorded work has
+// call after its last launch (an event record is a packet on the stream: one
+// per call, not one per buffer).  A new stream takes over the event of one whose recorded work has
 // completed once kMaxMarks streams are tracked, so the list stays bounded
 // however many short-lived streams a caller cycles through.
 constexpr size_t kMaxMarks = 16;
@@ -168,7 +167,13 @@ struct StreamMarks {
         }
     if (!slot) {
       hipEvent_t e = nullptr;
-      hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+      // device-scope release, no system-scope fence: the marks order streams
+      // of this device and tell the host that work has finished; none makes
+      // device writes visible to the host (callers' copies do that).  With
+      // the default system-scope fence a record cost ~5.7 us between two
+      // back-to-back steps (L2 written back and invalidated:
+      // profiles/r04/r04k_driver_cmd_timed_launches.txt).
+      hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence);
       if (r != hipSuccess) return (int32_t)r;
       marks.emplace_back(s, e);
       slot = &marks.back();

@@ -932,19 +932,34 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         // costs a v_and per word
 #pragma unroll
         for (int i = 0; i < CW; ++i) asm volatile("" : "+v"(d[i]), "+v"(cut[i]));
-        uint64_t bal[CW];
+        // per piece: the lanes with a flagged word (SALU) and the record's
+        // meta word with the flag bits (bit j = word j of the piece), formed
+        // word by word so that each word's flag mask dies at once (held for
+        // the appends, the eight masks pushed the unit's SGPRs into spills)
+        uint64_t ma = 0, mb = 0;
+        const uint32_t meta_a = meta_x | ((uint32_t)(ro + s * g.rstep) << 16);
+        uint32_t fa = meta_a, fb = meta_a + meta_b;
 #pragma unroll
         for (int i = 0; i < CW; ++i) {
-          uint64_t q0 = 0, q1 = 0;
+          uint64_t q0 = 0, q1 = 0, bal;
           if (MASKS) {
             select2(cw[i], d[i], cut[i], mm[i].x, mm[i].y, i < 4 ? vma : vmb, e[2 * i], e[2 * i + 1], q0, q1);
-            bal[i] = q0 | q1;
+            bal = q0 | q1;
           } else {
-            bal[i] = select2w(cw[i], d[i], cut[i], mm[i].x, mm[i].y, i < 4 ? vma : vmb, e[2 * i], e[2 * i + 1]);
+            bal = select2w(cw[i], d[i], cut[i], mm[i].x, mm[i].y, i < 4 ? vma : vmb, e[2 * i], e[2 * i + 1]);
           }
           // formed here, so the word's compare masks die here (sunk into the
           // append branches they would all stay live in SGPRs)
-          asm volatile("" : "+s"(bal[i]));
+          asm volatile("" : "+s"(bal));
+          if (i < 4) {
+            ma |= bal;
+            fa |= lane_bit(bal, 1u << i);
+            if (i & 1) asm volatile("" : "+v"(fa));  // (two words per v_or3)
+          } else {
+            mb |= bal;
+            fb |= lane_bit(bal, 1u << (i - 4));
+            if (i & 1) asm volatile("" : "+v"(fb));
+          }
           if (MASKS && (i < 4 ? valid : validb)) {  // verification mode: the exact path writes the flagged pixels
             const int y = y0 + s * g.rstep + (i < 4 ? 0 : half);
             uint8_t* mp = a.masks + ((int64_t)f * a.height + y) * a.width + x0 + xoff(i);
@@ -954,15 +969,6 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
             if (!__builtin_amdgcn_inverse_ballot_w64(q1)) mp[1] = a.mask_shift ? (uint8_t)(mp[1] | m1) : m1;
           }
         }
-        // per piece: the lanes with a flagged word (SALU) and the record's
-        // meta word with the flag bits (bit j = word j of the piece)
-        const uint64_t ma = bal[0] | bal[1] | bal[2] | bal[3];
-        const uint64_t mb = bal[4] | bal[5] | bal[6] | bal[7];
-        const uint32_t meta_a = meta_x | ((uint32_t)(ro + s * g.rstep) << 16);
-        const uint32_t fa = meta_a | lane_bit(bal[0], 1u) | lane_bit(bal[1], 2u) | lane_bit(bal[2], 4u) |
-                            lane_bit(bal[3], 8u);
-        const uint32_t fb = (meta_a + meta_b) | lane_bit(bal[4], 1u) | lane_bit(bal[5], 2u) | lane_bit(bal[6], 4u) |
-                            lane_bit(bal[7], 8u);
         u32x4 wa, wb;
         wa.x = cw[0]; wa.y = cw[1]; wa.z = cw[2]; wa.w = cw[3];
         wb.x = cw[4]; wb.y = cw[5]; wb.z = cw[6]; wb.w = cw[7];
