@@ -254,8 +254,12 @@ def main():
         total = world * F
         first, count = frame_shard(total, rank, world)
         assert count == F
+    # one non-blocking stream for the whole run (torch's default stream is the
+    # legacy null stream, whose launches synchronise with every other blocking
+    # stream on the device)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
     frames = torch.empty(max(F, 1) * fb, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream()
     trik_hsv.synth(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, args.kind, SEED, first_frame=first)
     hot = {"auto": trik_hsv.HOT_AUTO, "stripe": trik_hsv.HOT_STRIPE, "chroma": trik_hsv.HOT_CHROMA}[args.hot]
     det = trik_hsv.Detector(hot=hot)

@@ -352,6 +352,7 @@ struct TrikCvHandle {
   size_t d_maps_cap = 0;
   int maps_key[6] = {-1, -1, -1, -1, -1, -1};
   int32_t maps_rows2 = -1;  // first source row when the maps are the 2:1 ones, else -1
+  int32_t maps_guides = 0;  // the guide lines' output bits follow the maps (2:1 maps)
   int32_t maps_rows2_c0 = 0, maps_rows2_c1 = 0;  // the output columns the 2:1 maps write
   // the line sensors' overlay geometry on these maps (PreviewArgs::ovl_*)
   int32_t maps_ovl_half = 0, maps_ovl_ok = 0, maps_ovl_mag[4] = {-1, -1, -1, -1}, maps_ovl_band[2] = {-1, -1};
@@ -889,32 +890,66 @@ int32_t ensure_maps(TrikCvHandle* h, int w, int hgt, int ow, int oh, hipStream_t
     return 0;
   const size_t n = (size_t)w + hgt + ow + oh;
   h->maps_users.wait_all();  // previous users done
-  if (n > h->d_maps_cap) {
-    (void)hipFree(h->d_maps);
-    h->d_maps = nullptr; h->d_maps_cap = 0;
-    HIP_TRY(hipMalloc(&h->d_maps, sizeof(uint32_t) * (n ? n : 1)));
-    h->d_maps_cap = n;
-  }
   h->h_maps.assign(n ? n : 1, 0u);
   preview_maps(w, hgt, ow, oh, h->h_maps.data(), col_lo, col_hi);
-  HIP_TRY(hipMemcpyAsync(h->d_maps, h->h_maps.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice, s));
+  // the 2:1 maps (the defaults' 640x480 -> 320x240): preview_rows2_kernel
+  bool rows2 = false;
+  int c0 = 0, c1 = ow;
+  {
+    const uint32_t* last_row = h->h_maps.data() + w + hgt;
+    const uint32_t* last_col = last_row + oh;
+    rows2 = oh > 0 && ow > 0 && (int32_t)last_row[0] >= 0;
+    for (int r = 0; rows2 && r < oh; ++r) rows2 = (int32_t)last_row[r] == (int32_t)last_row[0] + 2 * r;
+    // the written columns: one window [c0, c1) with last_col[c] = 2c + 1, -1 outside
+    while (c0 < ow && (int32_t)last_col[c0] < 0) ++c0;
+    while (c1 > c0 && (int32_t)last_col[c1 - 1] < 0) --c1;
+    for (int c = 0; rows2 && c < ow; ++c)
+      rows2 = (c >= c0 && c < c1) ? (int32_t)last_col[c] == 2 * c + 1 : (int32_t)last_col[c] < 0;
+    h->maps_rows2 = rows2 ? (int32_t)last_row[0] : -1;
+  }
+  h->maps_rows2_c0 = c0;
+  h->maps_rows2_c1 = c1;
+  // The object sensors' 8 guide lines (draw_guides, WSEQ:136-166,471-485) as
+  // output pixels, one bit each, 8 per byte along a row, behind the maps: the
+  // 2:1 row kernel writes them as it writes the preview, so the overlay only
+  // draws the target circle.  The same points and clamping as Canvas::px.
+  h->maps_guides = 0;
+  if (rows2 && ow % 8 == 0 && w > 0 && hgt > 0) {
+    const size_t gpr = (size_t)ow / 8, words = ((size_t)oh * gpr + 3) / 4;
+    h->h_maps.resize(n + words, 0u);
+    uint8_t* bits = reinterpret_cast<uint8_t*>(h->h_maps.data() + n);
+    const uint32_t* wi2wo = h->h_maps.data();
+    const uint32_t* hi2ho = wi2wo + w;
+    const auto px = [&](int col, int row) {
+      const int sc = col < 0 ? 0 : (col > w - 1 ? w - 1 : col);
+      const int sr = row < 0 ? 0 : (row > hgt - 1 ? hgt - 1 : row);
+      const uint32_t oc = wi2wo[sc], orow = hi2ho[sr];
+      if (oc < (uint32_t)ow && orow < (uint32_t)oh) bits[orow * gpr + oc / 8] |= (uint8_t)(1u << (oc % 8));
+    };
+    const int step = hgt / 6, hh = hgt / 2, hw = w / 2;
+    for (int k = 0; k < 8 * 100; ++k) {
+      const int line = k / 100, adj = k % 100, off = (line & 3) < 2 ? ((line & 3) - 2) : ((line & 3) - 1);
+      if (line < 4) {
+        px(hw + off * step, hh - adj);
+        px(hw + off * step, hh + adj);
+      } else {
+        px(hw - adj, hh + off * step);
+        px(hw + adj, hh + off * step);
+      }
+    }
+    h->maps_guides = 1;
+  }
+  const size_t total = h->h_maps.size();
+  if (total > h->d_maps_cap) {
+    (void)hipFree(h->d_maps);
+    h->d_maps = nullptr; h->d_maps_cap = 0;
+    HIP_TRY(hipMalloc(&h->d_maps, sizeof(uint32_t) * total));
+    h->d_maps_cap = total;
+  }
+  HIP_TRY(hipMemcpyAsync(h->d_maps, h->h_maps.data(), sizeof(uint32_t) * total, hipMemcpyHostToDevice, s));
   HIP_TRY(hipStreamSynchronize(s));  // h_maps is pageable and reused
   h->maps_key[0] = w; h->maps_key[1] = hgt; h->maps_key[2] = ow; h->maps_key[3] = oh;
   h->maps_key[4] = col_lo; h->maps_key[5] = col_hi;
-  // the 2:1 maps (the defaults' 640x480 -> 320x240): preview_rows2_kernel
-  const uint32_t* last_row = h->h_maps.data() + w + hgt;
-  const uint32_t* last_col = last_row + oh;
-  bool rows2 = oh > 0 && ow > 0 && (int32_t)last_row[0] >= 0;
-  for (int r = 0; rows2 && r < oh; ++r) rows2 = (int32_t)last_row[r] == (int32_t)last_row[0] + 2 * r;
-  // the written columns: one window [c0, c1) with last_col[c] = 2c + 1, -1 outside
-  int c0 = 0, c1 = ow;
-  while (c0 < ow && (int32_t)last_col[c0] < 0) ++c0;
-  while (c1 > c0 && (int32_t)last_col[c1 - 1] < 0) --c1;
-  for (int c = 0; rows2 && c < ow; ++c)
-    rows2 = (c >= c0 && c < c1) ? (int32_t)last_col[c] == 2 * c + 1 : (int32_t)last_col[c] < 0;
-  h->maps_rows2 = rows2 ? (int32_t)last_row[0] : -1;
-  h->maps_rows2_c0 = c0;
-  h->maps_rows2_c1 = c1;
   // the line overlays' output pixels (line_overlay_kernel, LSEQ:419-474): a
   // column map with steps of 0 or 1 sends any source interval to one interval
   const uint32_t* wi2wo = h->h_maps.data();
@@ -959,6 +994,7 @@ PreviewArgs preview_args(const TrikCvHandle* h, const TrikHsvFrameBatch& b,
   a.last_row = reinterpret_cast<const int32_t*>(a.hi2ho + b.height);
   a.last_col = a.last_row + oh;
   a.rows2_first = h->maps_rows2;
+  if (h->maps_guides) a.guide_bits = reinterpret_cast<const uint8_t*>(h->d_maps + b.width + b.height + ow + oh);
   a.rows2_c0 = h->maps_rows2_c0;
   a.rows2_c1 = h->maps_rows2_c1;
   a.ovl_ok = h->maps_ovl_ok;

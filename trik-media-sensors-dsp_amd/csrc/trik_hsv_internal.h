@@ -210,6 +210,11 @@ struct PreviewArgs {
   // every output row and last_col[c] = 2 c + 1 for the output columns in
   // [rows2_c0, rows2_c1), -1 (not written) outside (preview_rows2_kernel)
   int32_t rows2_first = -1, rows2_c0 = 0, rows2_c1 = 0;
+  // the object sensors' guide lines as output bits ([out_h][out_w / 8], bit
+  // c % 8 of byte c / 8; 2:1 maps only, else NULL): the 2:1 kernel draws them
+  // as it writes the preview, and the overlay then draws only the circle
+  const uint8_t* guide_bits = nullptr;
+  int32_t guides_drawn = 0;  // set by launch_preview for the overlay
   // range 0 accepts every hue (its detect_mode() is not kDetectFull): the 2:1
   // kernel tests the sat&val mask alone
   int32_t hue_free = 0;

@@ -203,7 +203,7 @@ constexpr int kRowsQ = 1;  // units per lane and round (8 output pixels: 2 spill
 constexpr uint32_t rgb565x(uint32_t rgb) {  // write_px565's value
   return ((rgb >> 19) & 0x001fu) | ((rgb >> 5) & 0x07e0u) | ((rgb << 8) & 0xf800u);
 }
-template <int LAYOUT, bool WIN, bool HUEFREE, bool OVL = false>
+template <int LAYOUT, bool WIN, bool HUEFREE, bool OVL = false, bool GUIDES = false>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8)))
 void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
   using namespace stripe_px;
@@ -238,7 +238,7 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
     f += g.step_f + (cr ? 1u : 0u);
   };
   while (f < nf) {
-    uint32_t ff[kRowsQ], rr[kRowsQ], qq[kRowsQ], tpts[kRowsQ], tsx[kRowsQ];
+    uint32_t ff[kRowsQ], rr[kRowsQ], qq[kRowsQ], tpts[kRowsQ], tsx[kRowsQ], gbits[kRowsQ];
     u32x4 w[kRowsQ], wc[kRowsQ];
 #pragma unroll
     for (int u = 0; u < kRowsQ; ++u) {
@@ -253,6 +253,7 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
       }
       const uint8_t* src = a.frames + (int64_t)fl * a.frame_stride +
                            (int64_t)((uint32_t)a.rows2_first + 2u * r) * a.line_length + (YUYV ? 32 : 16) * (int64_t)q;
+      if (GUIDES) gbits[u] = a.guide_bits[r * gpr + q];  // (the same bytes for every frame: cached)
       w[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
       // YUYV: the unit's second piece; ov7670: its chroma bytes
       wc[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(YUYV ? src + 16 : src + plane));
@@ -317,6 +318,10 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
           v[k] = red ? rgb565x(0xff0000u) : (mag ? rgb565x(0xff00ffu) : v[k]);
         }
       }
+      if (GUIDES && gbits[u]) {  // the guide lines' pixels of this unit (draw_guides' colour)
+#pragma unroll
+        for (int k = 0; k < PX; ++k) v[k] = (gbits[u] >> k) & 1u ? rgb565x(0xff00ffu) : v[k];
+      }
       if (ff[u] < nf) {
         uint8_t* dst = a.previews + (int64_t)ff[u] * a.preview_stride + (int64_t)rr[u] * a.out_ll + 2 * PX * (int64_t)qq[u];
 #pragma unroll
@@ -341,7 +346,7 @@ __global__ __launch_bounds__(64) void overlay_kernel(PreviewArgs a, const TrikHs
   const int f = blockIdx.x, lane = threadIdx.x;
   const Canvas cv = stage_canvas<LDSMAP>(smaps, a.previews + (int64_t)f * a.preview_stride, a.out_ll, a.width,
                                          a.height, a.wi2wo, a.hi2ho, lane);
-  draw_guides(cv, lane, 64);  // WSEQ:471-485
+  if (!a.guides_drawn) draw_guides(cv, lane, 64);  // WSEQ:471-485 (else the 2:1 kernel drew them)
   __syncthreads();
   const TrikHsvTargetSums s = sums[(int64_t)f * sums_pitch];
   const uint32_t n = (uint32_t)s.points;
@@ -520,7 +525,7 @@ __global__ __launch_bounds__(kBlock) void auto_range_kernel(AutoRangeArgs a) {
 
 // The 2:1 row kernel when the maps, layout and alignment allow (see
 // preview_rows2_kernel); hipErrorNotSupported otherwise.
-static int launch_rows2(const PreviewArgs& a, hipStream_t s) {
+static int launch_rows2(const PreviewArgs& a, hipStream_t s, bool guides = false) {
   const bool yuyv = a.layout == TRIK_HSV_LAYOUT_YUYV;
   const int px = 8;  // output pixels per unit
   if (a.rows2_first < 0 || (!yuyv && a.layout != TRIK_HSV_LAYOUT_OV7670) || a.out_w % px || a.out_ll != 2 * a.out_w ||
@@ -555,7 +560,20 @@ static int launch_rows2(const PreviewArgs& a, hipStream_t s) {
         preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, false, true>},
        {preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, true, false>,
         preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, true, true>}}};
-  const Kern kern = ovl ? ovl_kerns[yuyv ? 0 : 1][win ? 1 : 0] : kerns[yuyv ? 0 : 1][win ? 1 : 0][hue_free ? 1 : 0];
+  // the object sensors' preview with its guide lines drawn in the same pass
+  static const Kern guide_kerns[2][2][2] = {
+      {{preview_rows2_kernel<TRIK_HSV_LAYOUT_YUYV, false, false, false, true>,
+        preview_rows2_kernel<TRIK_HSV_LAYOUT_YUYV, false, true, false, true>},
+       {preview_rows2_kernel<TRIK_HSV_LAYOUT_YUYV, true, false, false, true>,
+        preview_rows2_kernel<TRIK_HSV_LAYOUT_YUYV, true, true, false, true>}},
+      {{preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, false, false, false, true>,
+        preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, false, true, false, true>},
+       {preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, true, false, false, true>,
+        preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, true, true, false, true>}}};
+  if (guides && (ovl || a.meta || !a.guide_bits)) return hipErrorInvalidValue;
+  const Kern kern = ovl      ? ovl_kerns[yuyv ? 0 : 1][win ? 1 : 0]
+                    : guides ? guide_kerns[yuyv ? 0 : 1][win ? 1 : 0][hue_free ? 1 : 0]
+                             : kerns[yuyv ? 0 : 1][win ? 1 : 0][hue_free ? 1 : 0];
   hipError_t e = set_dynamic_lds(reinterpret_cast<const void*>(kern), 80 * 1024);
   if (e != hipSuccess) return e;
   PreviewRowsGeom g;
@@ -617,9 +635,16 @@ int launch_preview_body(const PreviewArgs& a, hipStream_t s) {
   return launch_gather(a, s);
 }
 
-int launch_preview(const PreviewArgs& a, const TrikHsvTargetSums* sums, int sums_pitch, hipStream_t s) {
-  if (a.n_frames <= 0 || a.out_w <= 0 || a.out_h <= 0) return hipSuccess;
-  hipError_t e = (hipError_t)launch_gather(a, s);
+int launch_preview(const PreviewArgs& pa, const TrikHsvTargetSums* sums, int sums_pitch, hipStream_t s) {
+  if (pa.n_frames <= 0 || pa.out_w <= 0 || pa.out_h <= 0) return hipSuccess;
+  PreviewArgs a = pa;
+  // the 2:1 row kernel draws the guide lines too where their bits exist
+  hipError_t e = hipErrorNotSupported;
+  if (a.guide_bits && !a.meta) {
+    e = (hipError_t)launch_rows2(a, s, true);
+    a.guides_drawn = e == hipSuccess ? 1 : 0;
+  }
+  if (e == hipErrorNotSupported) e = (hipError_t)launch_gather(a, s);
   if (e != hipSuccess || a.width <= 0 || a.height <= 0) return e;
   const size_t map_bytes = sizeof(uint32_t) * ((size_t)a.width + (size_t)a.height);
   if (map_bytes <= kMapLdsBytes)
