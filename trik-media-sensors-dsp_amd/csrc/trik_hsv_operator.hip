@@ -203,14 +203,16 @@ constexpr int kRowsQ = 1;  // units per lane and round (8 output pixels: 2 spill
 constexpr uint32_t rgb565x(uint32_t rgb) {  // write_px565's value
   return ((rgb >> 19) & 0x001fu) | ((rgb >> 5) & 0x07e0u) | ((rgb << 8) & 0xf800u);
 }
-template <int LAYOUT, bool WIN, bool HUEFREE, bool OVL = false, bool GUIDES = false>
+template <int LAYOUT, bool WIN, bool HUEFREE, bool OVL = false, bool GUIDES = false, bool META = false>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8)))
 void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
   using namespace stripe_px;
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   constexpr bool YUYV = LAYOUT == TRIK_HSV_LAYOUT_YUYV;
   constexpr int PX = 8;  // output pixels per unit
-  if (!a.meta) {
+  // (META: the multi-blob preview's metapixel flags as the detection, a
+  // template argument so that no other form computes their addresses)
+  if (!META) {
     const u32x4* src = reinterpret_cast<const u32x4*>(a.tables);
     typedef __attribute__((address_space(3))) u32x4* lds_u128_wptr;
     lds_u128_wptr dst = (lds_u128_wptr)(uintptr_t)0;
@@ -251,8 +253,10 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
         tpts[u] = ts[0];
         tsx[u] = ts[2];
       }
-      const uint8_t* src = a.frames + (int64_t)fl * a.frame_stride +
-                           (int64_t)((uint32_t)a.rows2_first + 2u * r) * a.line_length + (YUYV ? 32 : 16) * (int64_t)q;
+      // (32-bit offsets and one 64-bit multiply-add per address: launch_rows2
+      // checks that strides and in-frame offsets fit 32 bits, rows 24)
+      const uint8_t* src = a.frames + (uint64_t)fl * (uint32_t)a.frame_stride +
+                           (__umul24((uint32_t)a.rows2_first + 2u * r, (uint32_t)a.line_length) + (YUYV ? 32u : 16u) * q);
       if (GUIDES) gbits[u] = a.guide_bits[r * gpr + q];  // (the same bytes for every frame: cached)
       w[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
       // YUYV: the unit's second piece; ov7670: its chroma bytes
@@ -295,7 +299,7 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
         const Phase1 p = phase1<1>(ws[k], ws[k] ^ 0xFF00FF00u, m43_lane);  // the odd pixel: Y in byte 2
         const uint32_t c = PX * qq[u] + (uint32_t)k;                        // its output column
         uint32_t det;
-        if (a.meta) {
+        if (META) {
           const int64_t sr = (int64_t)a.rows2_first + 2 * (int64_t)rr[u];
           const int64_t sc = 2 * (int64_t)c + 1;
           det = a.meta[((int64_t)(ff[u] < nf ? ff[u] : 0u) * (a.height >> 2) + (sr >> 2)) * (a.width >> 2) +
@@ -323,7 +327,8 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
         for (int k = 0; k < PX; ++k) v[k] = (gbits[u] >> k) & 1u ? rgb565x(0xff00ffu) : v[k];
       }
       if (ff[u] < nf) {
-        uint8_t* dst = a.previews + (int64_t)ff[u] * a.preview_stride + (int64_t)rr[u] * a.out_ll + 2 * PX * (int64_t)qq[u];
+        uint8_t* dst = a.previews + (uint64_t)ff[u] * (uint32_t)a.preview_stride +
+                       (__umul24(rr[u], (uint32_t)a.out_ll) + 2u * PX * qq[u]);
 #pragma unroll
         for (int h = 0; h < PX / 4; ++h) {
           uint2 o;
@@ -543,6 +548,12 @@ static int launch_rows2(const PreviewArgs& a, hipStream_t s, bool guides = false
     return hipErrorNotSupported;
   const int64_t gpr = a.out_w / px, total = (int64_t)a.n_frames * a.out_h * gpr;
   if (total >= (1ll << 31)) return hipErrorNotSupported;
+  // the kernel's 32-bit strides and in-frame offsets, 24-bit row indices and line lengths
+  const int64_t frame_bytes = (int64_t)a.height * a.line_length * (yuyv ? 1 : 2);
+  if (a.frame_stride >= (1ll << 32) || a.preview_stride >= (1ll << 32) || frame_bytes >= (1ll << 32) ||
+      (int64_t)a.out_h * a.out_ll >= (1ll << 32) || a.line_length >= (1 << 24) || a.out_ll >= (1 << 24) ||
+      a.height >= (1 << 24))
+    return hipErrorNotSupported;
   if (total == 0) return hipSuccess;
   const bool win = a.rows2_c0 > 0 || a.rows2_c1 < a.out_w, hue_free = a.hue_free && !a.meta;
   const bool ovl = a.ovl_sums != nullptr;
@@ -571,7 +582,14 @@ static int launch_rows2(const PreviewArgs& a, hipStream_t s, bool guides = false
        {preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, true, false, false, true>,
         preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, true, true, false, true>}}};
   if (guides && (ovl || a.meta || !a.guide_bits)) return hipErrorInvalidValue;
+  // the multi-blob preview (metapixel flags)
+  static const Kern meta_kerns[2][2] = {
+      {preview_rows2_kernel<TRIK_HSV_LAYOUT_YUYV, false, false, false, false, true>,
+       preview_rows2_kernel<TRIK_HSV_LAYOUT_YUYV, true, false, false, false, true>},
+      {preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, false, false, false, false, true>,
+       preview_rows2_kernel<TRIK_HSV_LAYOUT_OV7670, true, false, false, false, true>}};
   const Kern kern = ovl      ? ovl_kerns[yuyv ? 0 : 1][win ? 1 : 0]
+                    : a.meta ? meta_kerns[yuyv ? 0 : 1][win ? 1 : 0]
                     : guides ? guide_kerns[yuyv ? 0 : 1][win ? 1 : 0][hue_free ? 1 : 0]
                              : kerns[yuyv ? 0 : 1][win ? 1 : 0][hue_free ? 1 : 0];
   hipError_t e = set_dynamic_lds(reinterpret_cast<const void*>(kern), 80 * 1024);
