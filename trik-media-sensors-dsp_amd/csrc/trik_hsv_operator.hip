@@ -200,6 +200,13 @@ struct PreviewRowsGeom {
   uint32_t step_f, step_r, step_q;  // the grid's lane count T as (frames, rows, groups)
 };
 constexpr int kRowsQ = 1;  // units per lane and round (8 output pixels: 2 spill at 64 VGPRs)
+// (m & a) | (~m & b): one v_bfi_b32 (in asm: LLVM turns the expression back
+// into two ANDs and an OR)
+__device__ __forceinline__ uint32_t bfi32(uint32_t m, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(m), "v"(a), "v"(b));
+  return r;
+}
 constexpr uint32_t rgb565x(uint32_t rgb) {  // write_px565's value
   return ((rgb >> 19) & 0x001fu) | ((rgb >> 5) & 0x07e0u) | ((rgb << 8) & 0xf800u);
 }
@@ -311,7 +318,9 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
           det = lds_u32(phase2_addr(m, p, hue_lane)) & sv & 1u;  // range 0 (combine keeps bit 0 in place)
         }
         // RGB565X of det ? 0x00ffff : rgb888 (WSEQ:316-354): R >> 3 | (G >> 2) << 5 | (B >> 3) << 11
-        const uint32_t c565 = ((uint32_t)p.r >> 3) | (((uint32_t)p.g & 0xFCu) << 3) | (((uint32_t)p.b & 0xF8u) << 8);
+        // (as two bitfield inserts: g << 3 keeps g's bits 2-7 in bits 5-10, b << 8
+        // its bits 3-7 in bits 11-15; r >> 3 has nothing above bit 4)
+        const uint32_t c565 = bfi32(0xF800u, (uint32_t)p.b << 8, bfi32(0x07E0u, (uint32_t)p.g << 3, (uint32_t)p.r >> 3));
         v[k] = det ? 0xFFE0u : c565;
         if (WIN) v[k] = c >= (uint32_t)a.rows2_c0 && c < (uint32_t)a.rows2_c1 ? v[k] : 0u;
         if (OVL) {  // thin lines (magenta) first, then the band and target lines (red) over them
