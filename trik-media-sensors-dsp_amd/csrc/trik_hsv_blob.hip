@@ -265,6 +265,22 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
       }
     }
     if (r + 1 < bh) load_row(r + 1, nx);
+    // a row without a set metapixel opens, joins and counts nothing (CLU:98-112
+    // only acts on set ones): its labels are 0 -- skip the scans (camera-like
+    // frames are mostly such rows)
+    {
+      uint32_t any = 0;
+#pragma unroll
+      for (int j = 0; j < KMAX; ++j) any |= dd[j];
+      if (__builtin_amdgcn_ballot_w64(any != 0u) == 0ull) {
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+          if (labels && j < K && c0 + j < bw) labels[(int64_t)r * bw + c0 + j] = 0;
+          prv[j] = 0;
+        }
+        continue;
+      }
+    }
     // the neighbours' boundary columns (CLU:70-84 reads c-1 and c+1)
     const uint32_t l_prev = from_prev_lane(prev_last, 0u), l_d = from_prev_lane(d_last, 0u);
     const uint32_t r_prev = from_next_lane(prv[0]);
