@@ -37,6 +37,8 @@
 //  blob_overlay_kernel  guide lines, then a 3x3 red mark per kept target.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "trik_hsv_internal.h"
 #include "trik_hsv_pixel.h"
 #include "trik_hsv_stripe_px.h"
@@ -187,7 +189,7 @@ __device__ __forceinline__ bool blob_target(int32_t size, int32_t sx, int32_t sy
 // guards fold away -- VGA's 160 metapixel columns are K = 3); the boundary
 // values of the neighbouring lanes come by one-lane shifts.  LDS holds eq
 // (and the staged bitmap).
-template <int KMAX, bool EXACT>
+template <int KMAX, bool EXACT, bool STAGED>
 __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
   extern __shared__ uint16_t smem[];
   const int f = blockIdx.x, lane = threadIdx.x;
@@ -195,12 +197,10 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
   const int ml = a.max_labels;
   uint16_t* eq = smem;  // [ml]
   // the frame's bitmap: staged in LDS when it fits (bw*bh is a multiple of 8)
-  const uint8_t* meta = a.meta + (int64_t)f * bw * bh;
-  if (a.meta_lds) {
+  if (STAGED) {
     uint32_t* dst = reinterpret_cast<uint32_t*>(eq + ((ml + 1) & ~1));
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(meta);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.meta + (int64_t)f * bw * bh);
     for (int i = lane; i < bw * bh / 4; i += 64) dst[i] = src[i];
-    meta = reinterpret_cast<const uint8_t*>(dst);
     __syncthreads();
   }
   // own statistics (zeroed by the launcher; folded in place at the end):
@@ -241,30 +241,65 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
 
   const int K = EXACT ? KMAX : (bw + 63) / 64;
   const int c0 = lane * K;
-  uint32_t prv[KMAX], cur[KMAX], dd[KMAX], up[KMAX], nx[KMAX];
+  uint32_t prv[KMAX], cur[KMAX], dd[KMAX], up[KMAX];
 #pragma unroll
   for (int j = 0; j < KMAX; ++j) prv[j] = 0;
   if (lane == 0) eq[0] = 0;
-  // this lane's columns of bitmap row r (loaded a row ahead: the loads of row
-  // r + 1 are in flight while row r is labelled)
-  auto load_row = [&](int r, uint32_t (&o)[KMAX]) {
-    const uint8_t* mrow = meta + (int64_t)r * bw;
+  // The bitmap rows come in batches of RB: batch b + 1's loads are in flight
+  // while batch b is labelled, and the wait for them comes once per batch.
+  // (Each wait is a full drain: the label stores and statistics atomics issued
+  // since are memory operations of another kind.  Waiting per row exposed a
+  // memory latency on every row, all of it on the empty rows of camera-like
+  // frames.)  bt: the current batch, row r's columns first (shifted up a row
+  // per row); pf: the next batch.  Loads take clamped columns and rows (no
+  // branches); columns past the row are masked when a batch is taken.
+  constexpr int RB = KMAX <= 5 ? 8 : 1;
+  uint32_t pf[RB][KMAX], bt[RB][KMAX];
+  // (LDS-staged or global: separate paths, so that neither is a flat load --
+  // a flat load in flight would hold every LDS wait of the row too)
+  // (the staged copy at its LDS offset: the dynamic LDS starts at 0)
+  typedef const __attribute__((address_space(3))) uint8_t* lds_u8_ptr;
+  typedef const __attribute__((address_space(1))) uint8_t* glb_u8_ptr;
+  const lds_u8_ptr meta_l = (lds_u8_ptr)(uintptr_t)(2u * (uint32_t)((ml + 1) & ~1));
+  const glb_u8_ptr meta_g = (glb_u8_ptr)(a.meta + (int64_t)f * bw * bh);
+  auto load_batch = [&](int r0) {
+    if (STAGED) {
 #pragma unroll
-    for (int j = 0; j < KMAX; ++j) o[j] = (j < K && c0 + j < bw) ? (uint32_t)mrow[c0 + j] : 0u;
+      for (int i = 0; i < RB; ++i)
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) pf[i][j] = meta_l[min(r0 + i, bh - 1) * bw + min(c0 + j, bw - 1)];
+    } else {
+#pragma unroll
+      for (int i = 0; i < RB; ++i)
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j)
+          pf[i][j] = meta_g[(int64_t)min(r0 + i, bh - 1) * bw + min(c0 + j, bw - 1)];
+    }
   };
-  if (bh > 0) load_row(0, nx);
+  if (bh > 0) load_batch(0);
   int next = 1;  // next new label (wave-uniform)
   for (int r = 0; r < bh; ++r) {
+    if (r % RB == 0) {  // take the batch in flight, start the next one
+#pragma unroll
+      for (int i = 0; i < RB; ++i)
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) bt[i][j] = (j < K && c0 + j < bw) ? pf[i][j] : 0u;
+      load_batch(r + RB);  // (unconditional: past the last row it re-reads it; a branch here
+                           // made the compiler copy, and so wait for, the new loads)
+    }
     uint32_t prev_last = 0, d_last = 0;
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) {
-      dd[j] = nx[j];
+      dd[j] = bt[0][j];
       if (j == K - 1) {
         prev_last = prv[j];
         d_last = dd[j];
       }
     }
-    if (r + 1 < bh) load_row(r + 1, nx);
+#pragma unroll
+    for (int i = 0; i + 1 < RB; ++i)
+#pragma unroll
+      for (int j = 0; j < KMAX; ++j) bt[i][j] = bt[i + 1][j];
     // a row without a set metapixel opens, joins and counts nothing (CLU:98-112
     // only acts on set ones): its labels are 0 -- skip the scans (camera-like
     // frames are mostly such rows)
@@ -560,10 +595,14 @@ int launch_blob(const BlobArgs& a, hipStream_t s) {
   b.meta_lds = a.n_frames < 2 * cus && lds + (size_t)bw * bh <= 40 * 1024 ? 1 : 0;
   if (b.meta_lds) lds += (size_t)bw * bh;
   const int K = (bw + 63) / 64;
-  auto kern = K == 1 ? blob_ccl_kernel<1, true> : K == 2 ? blob_ccl_kernel<2, true>
-            : K == 3 ? blob_ccl_kernel<3, true> : K == 4 ? blob_ccl_kernel<4, true>
-            : K == 5 ? blob_ccl_kernel<5, true> : K <= 8 ? blob_ccl_kernel<8, false>
-            : K <= 16 ? blob_ccl_kernel<16, false> : blob_ccl_kernel<32, false>;
+  auto pick = [&](auto staged) {
+    constexpr bool S = decltype(staged)::value;
+    return K == 1 ? blob_ccl_kernel<1, true, S> : K == 2 ? blob_ccl_kernel<2, true, S>
+         : K == 3 ? blob_ccl_kernel<3, true, S> : K == 4 ? blob_ccl_kernel<4, true, S>
+         : K == 5 ? blob_ccl_kernel<5, true, S> : K <= 8 ? blob_ccl_kernel<8, false, S>
+         : K <= 16 ? blob_ccl_kernel<16, false, S> : blob_ccl_kernel<32, false, S>;
+  };
+  auto kern = b.meta_lds ? pick(std::true_type{}) : pick(std::false_type{});
   hipLaunchKernelGGL(kern, dim3((unsigned)a.n_frames), dim3(64), lds, s, b);
   return hipGetLastError();
 }
