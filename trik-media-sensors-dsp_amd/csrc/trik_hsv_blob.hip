@@ -262,18 +262,16 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
   typedef const __attribute__((address_space(1))) uint8_t* glb_u8_ptr;
   const lds_u8_ptr meta_l = (lds_u8_ptr)(uintptr_t)(2u * (uint32_t)((ml + 1) & ~1));
   const glb_u8_ptr meta_g = (glb_u8_ptr)(a.meta + (int64_t)f * bw * bh);
+  uint32_t colc[KMAX];  // the lane's columns, clamped into the row
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j) colc[j] = (uint32_t)min(c0 + j, bw - 1);
   auto load_batch = [&](int r0) {
-    if (STAGED) {
 #pragma unroll
-      for (int i = 0; i < RB; ++i)
+    for (int i = 0; i < RB; ++i) {
+      const int rr = min(r0 + i, bh - 1);  // (wave-uniform: a scalar row base, the column as the offset)
 #pragma unroll
-        for (int j = 0; j < KMAX; ++j) pf[i][j] = meta_l[min(r0 + i, bh - 1) * bw + min(c0 + j, bw - 1)];
-    } else {
-#pragma unroll
-      for (int i = 0; i < RB; ++i)
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j)
-          pf[i][j] = meta_g[(int64_t)min(r0 + i, bh - 1) * bw + min(c0 + j, bw - 1)];
+      for (int j = 0; j < KMAX; ++j)
+        pf[i][j] = STAGED ? meta_l[(uint32_t)(rr * bw) + colc[j]] : (meta_g + (int64_t)rr * bw)[colc[j]];
     }
   };
   if (bh > 0) load_batch(0);
@@ -429,9 +427,11 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
           const uint32_t nb[4] = {j == 0 ? l_cur : cur[j > 0 ? j - 1 : 0],
                                   j == 0 ? l_prev : prv[j > 0 ? j - 1 : 0], prv[j],
                                   j + 1 < K ? prv[j + 1 < KMAX ? j + 1 : j] : r_prev};
+          // (unconditional: an absent neighbour (0) writes eq[0], which no
+          // scan step reads -- the writes go back to back, no branch and no
+          // wait between them)
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (nb[i]) eq[nb[i]] = e;
+          for (int i = 0; i < 4; ++i) eq[nb[i]] = e;
         }
       }
       __builtin_amdgcn_wave_barrier();
