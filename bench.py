@@ -85,6 +85,13 @@ def parse():
                     help="skip the cold-batch and scene measurements (PMC passes: only the bench's own launches)")
     ap.add_argument("--hot", choices=["auto", "stripe", "chroma"], default="auto",
                     help="hot kernel (auto = the library's choice: chroma-run for this batch size)")
+    ap.add_argument("--collective", choices=["comm", "torch"], default="comm",
+                    help="N > 1 over nccl: the totals' all-reduce through the library's own RCCL communicator "
+                         "(comm: trik_hsv_comm_all_reduce_totals, double-buffered on a second stream) or "
+                         "torch.distributed's (torch: in series on the step's stream)")
+    ap.add_argument("--comm-self", action="store_true",
+                    help="at N = 1 too: a library communicator of one rank, the same double-buffered "
+                         "all-reduce (exercises the N > 1 step's code path on one GPU)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="rocprofv3 FETCH_SIZE summary used for roofline.traffic (when measured on these sources)")
     args = ap.parse_args()
@@ -265,24 +272,71 @@ def main():
     det = trik_hsv.Detector(hot=hot)
     sums = torch.zeros((F, T, 3), dtype=torch.int64, device=dev)
     targets = torch.zeros((F, T, 4), dtype=torch.int8, device=dev)
-    totals = torch.zeros((T, 3), dtype=torch.int64, device=dev)
+    # the per-target totals, double-buffered: step k writes buffer k % 2, and
+    # its all-reduce (library comm) runs on a second stream while step k + 1's
+    # kernel runs; step k + 2 waits (device side) only for that all-reduce
+    totals_buf = [torch.zeros((T, 3), dtype=torch.int64, device=dev) for _ in range(2)]
+    totals = totals_buf[0]
 
-    def full_step(buf, rs, ev0=None, ev1=None):
+    # the collective: the library's own communicator when the
+    # ranks run over nccl (what a C++ host links), torch.distributed's on
+    # request, a host copy over gloo (rehearsal)
+    comm = None
+    if backend == "nccl" and (world > 1 or args.comm_self) and (args.collective == "comm" or world == 1):
+        uid = [trik_hsv.comm_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        comm = trik_hsv.Comm(world, rank, uid[0])
+    comm_stream = torch.cuda.Stream(device=dev) if comm is not None else None
+    kern_done = [torch.cuda.Event(), torch.cuda.Event()]
+    red_done = [None, None]
+    if comm is not None:
+        collective = {"call": "trik_hsv_comm_all_reduce_totals (the library's RCCL communicator, C ABI)",
+                      "ranks": world, "bytes": 24 * T,
+                      "overlap": "double-buffered totals: step k's all-reduce on a second stream while step "
+                                 "k+1's kernel runs; step k+2 waits for it on the device"}
+    elif world > 1 and backend == "nccl":
+        collective = {"call": "torch.distributed.all_reduce (RCCL)", "ranks": world, "bytes": 24 * T,
+                      "overlap": "none: in series after each step's kernel"}
+    elif world > 1:
+        collective = {"call": f"torch.distributed.all_reduce over {backend} on a host copy (rehearsal)",
+                      "ranks": world, "bytes": 24 * T, "overlap": "none"}
+    else:
+        collective = {"call": "none (one rank)", "ranks": 1}
+
+    def full_step(buf, rs, ev0=None, ev1=None, tot=None):
         """trik_hsv_process_batch_totals: sums, targets and totals of the batch
         (one chroma-run launch where the fused step applies), events around it."""
         if ev0 is not None:
             ev0.record(stream)
         det.process_batch_totals(buf, W, H, ll, trik_hsv.LAYOUT_YUYV, rs, n_frames=F, frame_stride=fb,
-                                 sums=sums, targets=targets, totals=totals, stream=stream)
+                                 sums=sums, targets=targets, totals=totals if tot is None else tot,
+                                 stream=stream)
         if ev1 is not None:
             ev1.record(stream)
 
+    nstep = [0]
+
     def step(ev0=None, ev1=None):
+        i = nstep[0] & 1
+        nstep[0] += 1
+        if comm is not None:
+            if red_done[i] is not None:  # the all-reduce that last read this buffer
+                stream.wait_event(red_done[i])
+            full_step(frames, ranges, ev0, ev1, tot=totals_buf[i])
+            kern_done[i].record(stream)
+            comm_stream.wait_event(kern_done[i])
+            comm.all_reduce_totals(totals_buf[i], stream=comm_stream)
+            if red_done[i] is None:
+                red_done[i] = torch.cuda.Event()
+            red_done[i].record(comm_stream)
+            return totals_buf[i]
         full_step(frames, ranges, ev0, ev1)
         if backend == "nccl":
-            all_reduce_totals(totals)  # RCCL over xGMI when N > 1: 3*T int64 per step
+            all_reduce_totals(totals)  # torch.distributed (RCCL) when N > 1: 3*T int64 per step
         elif world > 1:  # gloo rehearsal: reduce a host copy
             totals.copy_(all_reduce_totals(totals.cpu()))
+        return totals
 
     def timed_call(rs):
         """GPU time (HIP events on the stream) and host time of one full step."""
@@ -355,7 +409,9 @@ def main():
     # average duration, gaps between them included (an upper bound, and no
     # event packet between launches); otherwise event pairs around every 4th
     # step's launches
-    single_launch = det.last_hot_kernel() == trik_hsv.HOT_CHROMA and world == 1
+    # (one launch: the chroma-run kernel, one group of <= 4 ranges, one rank,
+    # no collective on the stream)
+    single_launch = det.last_hot_kernel() == trik_hsv.HOT_CHROMA and world == 1 and T <= 4 and comm is None
     every = args.event_every if args.event_every > 0 else (0 if single_launch else 4)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(0, args.steps, every)] if every else []
@@ -365,11 +421,14 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     region[0].record(stream)
+    last = totals
     for k in range(args.steps):
         if every and k % every == 0:
-            step(*evs[k // every])
+            last = step(*evs[k // every])
         else:
-            step()
+            last = step()
+    if comm is not None:  # the region ends with the last all-reduce
+        stream.wait_stream(comm_stream)
     region[1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -379,12 +438,18 @@ def main():
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs) if evs else region_ms
     # what the timed steps reduced: the totals after the last step against a
     # fresh sum of this rank's per-frame sums, reduced the same way
+    totals = last
     fresh = batch_totals(sums)
-    if backend == "nccl":
+    if comm is not None:
+        comm.all_reduce_totals(fresh, stream=stream)
+        torch.cuda.synchronize()
+    elif backend == "nccl":
         all_reduce_totals(fresh)
     elif world > 1:
         fresh = all_reduce_totals(fresh.cpu()).to(dev)
     totals_ok = bool(torch.equal(fresh, totals))
+    if comm is not None:  # the other buffer holds the step before's reduction: the same frames
+        totals_ok = totals_ok and bool(torch.equal(totals_buf[0], totals_buf[1]))
     ranks = dist.get_world_size() if world > 1 else 1
     kind = det.last_hot_kernel()
     kname = {trik_hsv.HOT_CHROMA: "chroma_kernel", trik_hsv.HOT_STRIPE: "stripe_kernel",
@@ -414,6 +479,7 @@ def main():
         "higher_is_better": True, "scaling": "strong" if args.total_frames else "weak", "vs_baseline": None,
         "dtype": "u8", "ranks": ranks, "backend": (("nccl (RCCL)" if backend == "nccl" else backend)
                                                   if world > 1 else "none (one process)"),
+        "collective": collective,
         "totals_check": {"ok": totals_ok, "frames_reduced": total,
                          "points": [int(x) for x in totals[:, 0].tolist()],
                          "how": "after the timed steps, a fresh sum of the rank's per-frame sums, "
@@ -429,7 +495,8 @@ def main():
                      "kernel": f"{kname}<YUYV,{T}>", "kernel_ms": round(kern_ms, 4),
                      "kernel_ms_max_rank": round(kern_ms_max, 4),
                      "kernel_ms_how": ("one event pair around the timed region / steps (each step is this one "
-                                       "launch)" if not evs else
+                                       "launch plus the library's stream mark and, every 8th call, its 8-byte "
+                                       "AUTO probe readback; the gaps between launches included)" if not evs else
                                        f"event pairs around every {every}-th step's launches ({len(evs)} steps)"),
                      "region_ms_per_step": round(region_ms, 4),
                      "kernel_scope": ("the step's one launch (fused: its frames' sums zeroed and added, targets and totals written "
@@ -460,6 +527,8 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     det.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -6,7 +6,9 @@ chromas), to place and check the AUTO selector (development only).
 usage (GPU box): python scripts/adversarial_ranges.py [frames]
 One line per case: the builder's expected flagged-word share (uniform
 input), the measured share of the frames where it differs, then each
-hot-kernel setting's kernel and ms per batch (trik_hsv_batch_sums, HIP events).
+hot-kernel setting's kernel and ms per batch (trik_hsv_batch_sums, HIP events;
+median of 3 passes in rotated order, 40 synchronised warm-up calls per
+setting and pass).
 """
 import os
 import sys
@@ -70,34 +72,56 @@ def concentrated_frames(F, W, H, kinds, seed=5):
     return words.astype("<u4").view(np.uint8), share
 
 
-def time_case(frames, F, W, H, ranges, reps=20):
+def time_case(frames, F, W, H, ranges, reps=20, warm=40, passes=3, seed=0):
+    """Each hot-kernel setting on its own handle (AUTO's measured-share state
+    is per handle), all built before any timing; then `passes` passes, each
+    in a rotated order (pass p starts at setting p), every setting given the
+    same `warm` synchronised warm-up calls before its `reps` timed calls (HIP
+    events); the median over the passes.  (Round 4's table timed the settings
+    in a fixed order -- forced chroma right after the cold table build with 5
+    warm-ups, AUTO last with 40 -- so clock transients decided the ratios.)"""
     ll = 2 * W
     stream = torch.cuda.current_stream()
-    det = trik_hsv.Detector()
+    kinds = (trik_hsv.HOT_CHROMA, trik_hsv.HOT_STRIPE, trik_hsv.HOT_AUTO)
+    dets = {}
     sums = torch.zeros((F, len(ranges), 3), dtype=torch.int64, device=frames.device)
-    out, expected = [], None
-    for hot in (trik_hsv.HOT_CHROMA, trik_hsv.HOT_STRIPE, trik_hsv.HOT_AUTO):
-        det.set_hot_kernel(hot)
+    expected = None
+    for hot in kinds:
+        det = trik_hsv.Detector(hot=hot)
         det.batch_sums(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, ranges, sums, stream=stream)
+        torch.cuda.synchronize()
         if hot == trik_hsv.HOT_CHROMA:
             expected = det.chroma_flagged_share()
-        # warm-up, synchronised per call: AUTO reads the measured share back
-        # every few launches (trik_hsv_abi.cpp: probe_measured / poll_measured)
-        for _ in range(5 if hot != trik_hsv.HOT_AUTO else 40):
-            det.batch_sums(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, ranges, sums, stream=stream)
+        dets[hot] = det
+    times = {hot: [] for hot in kinds}
+    ran = {}
+    for p in range(passes):
+        order = kinds[p % 3:] + kinds[:p % 3]
+        for hot in order:
+            det = dets[hot]
+            # warm-up, synchronised per call: AUTO reads the measured share
+            # back every few launches (trik_hsv_abi.cpp: probe_measured)
+            for _ in range(warm):
+                det.batch_sums(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, ranges, sums, stream=stream)
+                torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                det.batch_sums(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, ranges, sums, stream=stream)
+            e1.record(stream)
             torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(reps):
-            det.batch_sums(frames, W, H, ll, trik_hsv.LAYOUT_YUYV, ranges, sums, stream=stream)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        ran = {trik_hsv.HOT_CHROMA: "chroma", trik_hsv.HOT_STRIPE: "stripe",
-               trik_hsv.HOT_MIXED: "mixed"}.get(det.last_hot_kernel(), "?")
-        if hot == trik_hsv.HOT_AUTO:
-            ran += f"[m={det.chroma_measured_share():.3f}]"
-        out.append((["auto", "stripe", "chroma"][hot], ran, e0.elapsed_time(e1) / reps))
-    det.close()
+            times[hot].append(e0.elapsed_time(e1) / reps)
+            r = {trik_hsv.HOT_CHROMA: "chroma", trik_hsv.HOT_STRIPE: "stripe",
+                 trik_hsv.HOT_MIXED: "mixed"}.get(det.last_hot_kernel(), "?")
+            if hot == trik_hsv.HOT_AUTO:
+                r += f"[m={det.chroma_measured_share():.3f}]"
+            ran[hot] = r
+    out = []
+    for hot in kinds:
+        t = sorted(times[hot])
+        out.append((["auto", "stripe", "chroma"][hot], ran[hot], t[len(t) // 2]))
+    for det in dets.values():
+        det.close()
     return expected, out
 
 

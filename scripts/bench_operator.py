@@ -73,7 +73,7 @@ def main():
                       "bytes_algorithmic": pv_bytes,
                       "achieved_GBs": round(pv_bytes / (pv_ms / 1e3) / 1e9, 1),
                       "hbm_frac": round(pv_bytes / (pv_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                      "note": "preview_gather_kernel (writes every preview byte) + overlay_kernel"}
+                      "note": "preview_rows2_kernel (the 2:1 map: writes every preview byte, guide lines included) + overlay_kernel (the target circle)"}
 
     ar_ms = timed(lambda: trik_hsv.batch_auto_range(dev, W, H, LL, trik_hsv.LAYOUT_YUYV), stream,
                   args.iters)
@@ -91,7 +91,7 @@ def main():
                    "bytes_algorithmic": lf * lfb,
                    "achieved_GBs": round(lf * lfb / (ln_ms / 1e3) / 1e9, 1),
                    "hbm_frac": round(lf * lfb / (ln_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                   "note": "line_sums_kernel + line_targets_kernel"}
+                   "note": "line_vec_kernel + line_targets_kernel"}
     lsums, _ = trik_hsv.line_batch(ldev, W, H, W, 0, 30)
     lp_ms = timed(lambda: det.line_preview(ldev, W, H, W, 0, 30, lsums, out_width=OW, out_height=OH,
                                            out_line_length=OLL), stream, args.iters)

@@ -133,3 +133,21 @@ def test_auto_wide_rows_cold_set_counts_once(torch_dev, hsv, oracle_mod):
             assert (sums.cpu().numpy() == want).all()
     finally:
         d.close()
+
+
+def test_empty_batch_keeps_gated_answer(torch_dev, hsv):
+    """a first batch of a new range set is planned on the device
+    (gated launches: the builder's cost is not back yet); an empty batch after
+    it must keep that call's answer, and last_hot_kernel() resolve it to a
+    valid kind (it returned the negative partner code when the empty call
+    dropped the pending set)."""
+    torch = torch_dev
+    n = 64
+    frames = torch.empty(n * H * LL, dtype=torch.uint8, device="cuda")
+    hsv.synth(frames, W, H, LL, LAYOUT_YUYV, 0, 0x7A1C)
+    det = hsv.Detector()
+    det.process_batch(frames, W, H, LL, LAYOUT_YUYV, BENCH_RANGES)
+    det.process_batch(frames, W, H, LL, LAYOUT_YUYV, BENCH_RANGES, n_frames=0)
+    torch.cuda.synchronize()
+    assert det.last_hot_kernel() == hsv.HOT_CHROMA
+    det.close()

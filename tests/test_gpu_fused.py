@@ -2,7 +2,7 @@
 splits the batch's units evenly over its workgroups, and the wave that counts
 a frame's last unit stores the frame's sums and targets; the last workgroup
 writes the per-target batch totals -- one launch (trik_hsv_chroma.hip:
-chroma_kernel, chroma_fused_ok; DESIGN.md section 4.1).
+chroma_kernel, chroma_fused_ok; DESIGN.md section 4.5).
 
 Held to the separate-kernel path (the hot kernel adding into zeroed sums,
 then the epilogue and totals kernels) bit for bit, and to the oracle

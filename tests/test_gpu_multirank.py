@@ -101,6 +101,7 @@ def test_bench_two_ranks_rehearsal(extra):
     # the line proves what it measured: the process group's size, its backend,
     # and the reduced totals equal to a fresh reduction of the per-frame sums
     assert d["ranks"] == 2 and d["backend"] == "gloo"
+    assert d["collective"]["ranks"] == 2 and "gloo" in d["collective"]["call"]
     chk = d["totals_check"]
     assert chk["ok"] is True and chk["frames_reduced"] == d["config"]["frames_total"]
     assert len(chk["points"]) == d["config"]["targets"] and all(p > 0 for p in chk["points"])
@@ -108,3 +109,21 @@ def test_bench_two_ranks_rehearsal(extra):
         assert d["scaling"] == "strong" and d["config"]["frames_total"] == 97
     else:
         assert d["scaling"] == "weak" and d["config"]["frames_total"] == 128
+
+
+def test_bench_library_comm_one_rank():
+    """bench.py's N > 1 collective path on one GPU (--comm-self): the totals
+    all-reduced through the library's own communicator
+    (trik_hsv_comm_all_reduce_totals, a comm of one rank), double-buffered on a
+    second stream; the line names the call and its totals check holds."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "6", "--warmup", "3", "--frames", "64",
+           "--no-cpu-baseline", "--no-extras", "--comm-self"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["collective"]["call"].startswith("trik_hsv_comm_all_reduce_totals")
+    assert "double-buffered" in d["collective"]["overlap"]
+    chk = d["totals_check"]
+    assert chk["ok"] is True and chk["frames_reduced"] == 64 and all(p > 0 for p in chk["points"])

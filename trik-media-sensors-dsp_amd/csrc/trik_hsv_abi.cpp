@@ -510,6 +510,21 @@ int32_t setup_dynamic(TrikCvHandle* h, const TRIK_VIDTRANSCODE_CV_DynamicParams*
   return setup_image_desc(h);
 }
 
+// The last call's gated groups (hot_groups[g] = -partner: AUTO's choice made
+// on the device from the builder cost) resolved from that cost, which was
+// copied back without a host wait: waits for the copy.  Runs when the answer
+// is asked for and before the pending set's slot is reused.
+void resolve_pending(TrikCvHandle* h) {
+  TableSet* t = h->pending_set;
+  if (!t) return;
+  (void)hipEventSynchronize(t->cost_ready);
+  for (size_t g = 0; g < h->hot_groups.size(); ++g)
+    if (h->hot_groups[g] < 0)
+      h->hot_groups[g] = (int8_t)(g < (size_t)t->groups_cap && t->h_cost[g] <= kChromaMaxCost ? TRIK_HSV_HOT_CHROMA
+                                                                                             : -h->hot_groups[g]);
+  h->pending_set = nullptr;
+}
+
 // The tables for ranges[0..n), stream-ordered on s: a cached set (s waits
 // for its uploads, device side), or a set compiled now into a slot whose
 // earlier uses have completed -- found without blocking (hipEventQuery);
@@ -543,7 +558,7 @@ int32_t acquire_tables(TrikCvHandle* h, const TRIK_VIDTRANSCODE_CV_InArgsAlg* ra
     v->users.wait_all();
     if (v->ready) HIP_TRY(hipEventSynchronize(v->ready));
   }
-  if (h->pending_set == v) h->pending_set = nullptr;
+  if (h->pending_set == v) resolve_pending(h);  // (its costs are about to be overwritten)
   if (h->sums_set == v) h->sums_set = nullptr;
   const int groups = (n + kRangesPerLaunch - 1) / kRangesPerLaunch;
   if (groups > v->groups_cap) {
@@ -864,7 +879,8 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
     }
     HIP_TRY(e);
   }
-  h->pending_set = gated ? t : nullptr;
+  // (an empty batch keeps the last call's answer, gated groups included)
+  if (!args.empty()) h->pending_set = gated ? t : nullptr;
   if (chroma_ran) ++t->chroma_runs;  // once per call, whichever groups ran it
   if (!masks) {
     rc = probe_measured(*t, reprobe, s);
@@ -1707,16 +1723,9 @@ extern "C" int32_t trik_hsv_set_hot_kernel(TRIK_VIDTRANSCODE_CV_Handle h, int32_
 extern "C" int32_t trik_hsv_last_hot_kernel(TRIK_VIDTRANSCODE_CV_Handle h) {
   if (!h) return 0;
   std::lock_guard<std::mutex> lock(h->mu);
-  if (h->pending_set) {  // the device chose: resolve each gated group from its builder cost
+  {
     DeviceGuard dg(h->device);
-    TableSet* t = h->pending_set;
-    (void)hipEventSynchronize(t->cost_ready);
-    for (size_t g = 0; g < h->hot_groups.size(); ++g)
-      if (h->hot_groups[g] < 0)
-        h->hot_groups[g] = (int8_t)(g < (size_t)t->groups_cap && t->h_cost[g] <= kChromaMaxCost
-                                        ? TRIK_HSV_HOT_CHROMA
-                                        : -h->hot_groups[g]);
-    h->pending_set = nullptr;
+    resolve_pending(h);
   }
   int kind = 0;
   for (int8_t k : h->hot_groups) {

@@ -411,6 +411,58 @@ class Group:
         self.close()
 
 
+COMM_ID_BYTES = 128  # TRIK_HSV_COMM_ID_BYTES (= NCCL_UNIQUE_ID_BYTES)
+
+
+def comm_id() -> bytes:
+    """A fresh communicator id (rank 0 makes it; every rank passes the same
+    bytes to Comm): trik_hsv_comm_id."""
+    buf = (C.c_uint8 * COMM_ID_BYTES)()
+    rc = _lib.trik_hsv_comm_id(buf)
+    if rc:
+        raise TrikHsvError(rc, "trik_hsv_comm_id")
+    return bytes(buf)
+
+
+class Comm:
+    """One process per GPU: the library's own RCCL communicator over the ranks
+    (trik_hsv_comm_create on the current device) and its one collective, the
+    sum of the per-target totals (trik_hsv_comm_all_reduce_totals) -- the call
+    a C++ host links, not torch.distributed's."""
+
+    def __init__(self, n_ranks: int, rank: int, uid: bytes):
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError(f"comm id must be {COMM_ID_BYTES} bytes")
+        buf = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        rc = _lib.trik_hsv_comm_create(int(n_ranks), int(rank), buf, C.byref(h))
+        if rc:
+            raise TrikHsvError(rc, "trik_hsv_comm_create")
+        self._h = h
+        self.n_ranks, self.rank = int(n_ranks), int(rank)
+
+    def all_reduce_totals(self, totals, *, stream=None):
+        """Sum totals [T, 3] int64 (device) over the ranks in place, enqueued
+        on `stream` (default: torch's current stream)."""
+        import torch
+
+        if totals.dtype != torch.int64 or totals.dim() != 2 or totals.shape[1] != 3 or not totals.is_contiguous():
+            raise ValueError("totals must be a contiguous [T, 3] int64 device tensor")
+        rc = _lib.trik_hsv_comm_all_reduce_totals(self._h, C.c_void_p(totals.data_ptr()), int(totals.shape[0]),
+                                                  _stream_ptr(stream, totals))
+        if rc:
+            raise TrikHsvError(rc, "trik_hsv_comm_all_reduce_totals")
+        return totals
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.trik_hsv_comm_delete(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
 def synth(frames, width, height, line_length, layout, kind, seed, *, first_frame=0, n_frames=None,
           frame_stride=None, stream=None):
     """Fill a uint8 device tensor with synthetic frames (kind 0 uniform, 1 scene)."""
