@@ -21,8 +21,9 @@
 //    shape costs only the pixels in its window.  The exception code
 //    kChromaExc flags both pixels of the word.
 //  * The hot loop per YUYV word: one v_perm for c, three LDS reads (run
-//    descriptor, block masks, the byte-spread mask pair), five compares and
-//    four selects; the flags are SALU operations on the compare masks.
+//    descriptor, block word, the byte-spread mask pair), seven compares
+//    (exception code; Y0/Y1 < b1, <= b2, >= the block's cut) and four
+//    selects; the flags are SALU operations on the compare masks.
 //    Accumulation is the stripe kernel's (byte-packed per-lane counters,
 //    lanes own chunk columns and walk rows).
 //  * Flagged words are compacted into a per-wave LDS queue (ballot + mbcnt);
@@ -35,6 +36,12 @@
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
+
+// gfx950 only: the fused step's completion protocol relies on GFX9 memory
+// counters (vmcnt counts atomics without return; no separate store counter)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "trik_hsv_chroma.hip targets gfx950 only"
+#endif
 
 #include "trik_hsv_internal.h"
 #include "trik_hsv_pixel.h"
@@ -748,6 +755,13 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
   };
   auto count_done = [&]() {  // the last emitted unit, once its atomics are performed
     if (pend_f < 0) return;
+    // The release between this wave's relaxed accumulator adds and its
+    // relaxed count add: on gfx950 (GFX9 counters) vmcnt also counts atomics
+    // without return, and device-scope atomics execute at the memory side, so
+    // once vmcnt is 0 the adds are performed for every later atomic (the
+    // finalizing wave's atomicExch included).  A release fence would also
+    // write back this CU's L2 lines (buffer_wbl2) at every unit end.  The
+    // file is gfx950-only (see the guard at the top).
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t r = 0;
     if (lane == 0) r = atomicAdd(reinterpret_cast<uint32_t*>(a.frame_acc + 16 * (int64_t)pend_f + 12), 1u);
