@@ -243,6 +243,16 @@ int main(int argc, char** argv) {
            "workgroup end min/p50/max %.1f/%.1f/%.1f us\n",
            L.path.c_str(), nwg, pct(spread, 0.5), pct(spread, 0.9), pct(spread, 1.0), pct(lastv, 0.0), pct(lastv, 0.5),
            pct(lastv, 1.0));
+    // workgroup end by XCD (blockIdx % 8 under round-robin placement) and the
+    // units each workgroup's waves took
+    printf("%-40s trace: workgroup end by blockIdx %% 8 (p50/max):", L.path.c_str());
+    for (int x = 0; x < 8; ++x) {
+      std::vector<double> v;
+      for (int g = x; g < nwg; g += 8)
+        if (wlast[g] > 0) v.push_back(wlast[g]);
+      if (!v.empty()) printf(" %d:%.1f/%.1f", x, pct(v, 0.5), pct(v, 1.0));
+    }
+    printf("\n");
   }
   const double bytes = (double)fb * frames;
   for (Lib& L : libs) {

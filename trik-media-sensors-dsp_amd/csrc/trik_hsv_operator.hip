@@ -535,6 +535,190 @@ __global__ __launch_bounds__(kBlock) void auto_range_kernel(AutoRangeArgs a) {
   }
 }
 
+// autoDetectHsv on 16-byte aligned batches (frames, frame stride and line
+// length): the same result as auto_range_kernel, organised for throughput.
+//  * The zone is cut into 16-byte chunks of its rows (YUYV: 4 words = 8
+//    pixels; ov7670: 16 luma + 16 chroma bytes = 16 pixels); a lane takes
+//    chunks tid, tid + 256, ... in batches of kVecBatch with every load of a
+//    batch in flight (the one-pixel-per-lane walk waited one load latency per
+//    pixel).
+//  * Pass 1 counts only: a lane run-length encodes the (H, S, V) triples of
+//    its pixels in scan order and adds each run once per channel to its
+//    wave's LDS histograms (one atomic per run, not per pixel).
+//  * The winner of a channel whose maximum count M is held by one value is
+//    that value.  Only channels where several values reach M need their last
+//    occurrences (see the file comment): pass 2 recomputes the zone's HSV and
+//    takes atomicMax of the scan position for pixels of those values alone.
+constexpr int kVecBatch = 4;
+struct AutoVecGeom {
+  int32_t r0, c0, c1;  // zone rows [r0, r0 + rows), pixel columns [c0, c1)
+  int32_t k0;          // first chunk column
+  FastDiv per_row;     // chunks per zone row
+  uint32_t total;      // zone rows * chunks per row
+};
+
+// (H | S << 8 | V << 16) of pixel P of the YUYV-ordered word w (Y0 U Y1 V):
+// hsv_bytes' arithmetic on a word in registers
+template <int P>
+__device__ __forceinline__ uint32_t hsv_key(uint32_t w, const uint16_t* l43, const uint16_t* l255) {
+  using stripe_px::clamp8_shift6;
+  constexpr uint32_t kY = P == 0 ? 74u : (74u << 16);
+  const uint32_t wc = w ^ 0xFF00FF00u;
+  const int r = clamp8_shift6(__builtin_amdgcn_udot4(w, kY | (102u << 24), (uint32_t)-14248, false));
+  const int g = clamp8_shift6(__builtin_amdgcn_udot4(wc, kY | (25u << 8) | (52u << 24), (uint32_t)-10939, false));
+  const int b = clamp8_shift6(__builtin_amdgcn_udot4(w, kY | (129u << 8), (uint32_t)-17672, false));
+  const int mx = max(r, max(g, b)), mn = min(r, min(g, b));
+  const bool eqG = mx == g, eqB = mx == b;  // priority G > B > R (WSEQ:226-246)
+  const int diff = eqG ? b - r : (eqB ? r - g : g - b);
+  const int base = eqG ? 21845 : (eqB ? 43690 : 0);
+  const uint32_t h = (((uint32_t)(base + (int)l43[mx - mn] * diff)) >> 8) & 0xFFu;
+  const uint32_t s = ((uint32_t)l255[mx] * (uint32_t)(mx - mn)) >> 8;
+  return h | (s << 8) | ((uint32_t)mx << 16);
+}
+
+template <int LAYOUT>
+__global__ __launch_bounds__(kRangeBlock) void auto_range_vec_kernel(AutoRangeArgs a, AutoVecGeom g) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  constexpr int kWaves = kRangeBlock / 64;
+  constexpr bool YUYV = LAYOUT == TRIK_HSV_LAYOUT_YUYV;
+  constexpr int NW = YUYV ? 4 : 8;  // words (pixel pairs) per chunk
+  __shared__ uint32_t cnt[kWaves][3][256];
+  __shared__ uint32_t lst[3][256];
+  __shared__ uint32_t top_n[3], n_top[3];
+  __shared__ unsigned long long best[3];
+  __shared__ uint16_t l43[256], l255[256];
+  const int f = blockIdx.x, tid = threadIdx.x, wave = tid >> 6;
+  for (int i = tid; i < kWaves * 3 * 256; i += kRangeBlock) (&cnt[0][0][0])[i] = 0;
+  for (int i = tid; i < 3 * 256; i += kRangeBlock) (&lst[0][0])[i] = 0;
+  for (int i = tid; i < 256; i += kRangeBlock) {
+    l43[i] = c_luts.l43[i];
+    l255[i] = c_luts.l255[i];
+  }
+  if (tid < 3) {
+    top_n[tid] = 0;
+    n_top[tid] = 0;
+    best[tid] = ~0ull;
+  }
+  __syncthreads();
+  const uint8_t* fr = a.frames + (int64_t)f * a.frame_stride;
+  const int64_t plane = (int64_t)a.height * a.line_length;
+  // one batch of chunks: their words (a chunk past the zone re-reads the
+  // lane's first chunk and is masked), rows and first pixel columns
+  auto load_batch = [&](uint32_t j0, uint32_t (&w)[kVecBatch][NW], int (&row)[kVecBatch], int (&x0)[kVecBatch],
+                        bool (&ok)[kVecBatch]) {
+#pragma unroll
+    for (int b = 0; b < kVecBatch; ++b) {
+      const uint32_t j = j0 + (uint32_t)(b * kRangeBlock);
+      ok[b] = j < g.total;
+      const uint32_t jj = ok[b] ? j : (uint32_t)tid;
+      const uint32_t zr = fdiv(jj, g.per_row);
+      const uint32_t kc = (uint32_t)g.k0 + (jj - zr * g.per_row.d);
+      row[b] = g.r0 + (int)zr;
+      x0[b] = (int)kc * 2 * NW;
+      const uint8_t* p = fr + (int64_t)row[b] * a.line_length + 16 * (int64_t)kc;
+      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+      if (YUYV) {
+        w[b][0] = v.x; w[b][1] = v.y; w[b][2] = v.z; w[b][3] = v.w;
+      } else {  // 16 luma bytes, 16 chroma bytes: words (Y0, U = odd chroma, Y1, V = even chroma)
+        const u32x4 c = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + plane));
+        const uint32_t yy[4] = {v.x, v.y, v.z, v.w}, cc[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          w[b][2 * k] = __builtin_amdgcn_perm(cc[k], yy[k], 0x04010500u);
+          w[b][2 * k + 1] = __builtin_amdgcn_perm(cc[k], yy[k], 0x06030702u);
+        }
+      }
+    }
+  };
+  // the zone's pixels of this lane, in scan order, through fn(key, pos)
+  auto walk = [&](auto fn) {
+    for (uint32_t j0 = (uint32_t)tid; j0 < g.total; j0 += kVecBatch * kRangeBlock) {
+      uint32_t w[kVecBatch][NW];
+      int row[kVecBatch], x0[kVecBatch];
+      bool ok[kVecBatch];
+      load_batch(j0, w, row, x0, ok);
+#pragma unroll
+      for (int b = 0; b < kVecBatch; ++b) {
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+          const int c = x0[b] + 2 * i;
+          const uint32_t pos = (uint32_t)row[b] * (uint32_t)a.width + (uint32_t)c;
+          const uint32_t k0 = hsv_key<0>(w[b][i], l43, l255), k1 = hsv_key<1>(w[b][i], l43, l255);
+          if (ok[b] && c >= g.c0 && c < g.c1) fn(k0, pos);
+          if (ok[b] && c + 1 >= g.c0 && c + 1 < g.c1) fn(k1, pos + 1u);
+        }
+      }
+    }
+  };
+  // pass 1: run-length encoded counts
+  uint32_t rk = 0u, rl = 0u;
+  auto flush = [&]() {
+    if (rl) {
+      atomicAdd(&cnt[wave][0][rk & 0xFFu], rl);
+      atomicAdd(&cnt[wave][1][(rk >> 8) & 0xFFu], rl);
+      atomicAdd(&cnt[wave][2][rk >> 16], rl);
+    }
+  };
+  walk([&](uint32_t key, uint32_t) {
+    if (rl && key == rk) {
+      ++rl;
+    } else {
+      flush();
+      rk = key;
+      rl = 1u;
+    }
+  });
+  flush();
+  __syncthreads();
+  for (int i = tid; i < 3 * 256; i += kRangeBlock) {
+    uint32_t n = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) n += (&cnt[w][0][0])[i];
+    (&cnt[0][0][0])[i] = n;
+    if (n) atomicMax(&top_n[i >> 8], n);
+  }
+  __syncthreads();
+  for (int i = tid; i < 3 * 256; i += kRangeBlock) {
+    const int k = i >> 8;
+    const uint32_t n = (&cnt[0][0][0])[i];
+    if (n && n == top_n[k]) {
+      atomicAdd(&n_top[k], 1u);
+      atomicMin(&best[k], (unsigned long long)(i & 255));
+    }
+  }
+  __syncthreads();
+  const uint32_t tie = (n_top[0] > 1u ? 1u : 0u) | (n_top[1] > 1u ? 2u : 0u) | (n_top[2] > 1u ? 4u : 0u);
+  if (tie) {  // (workgroup-uniform) pass 2: the last occurrences of the tied values
+    walk([&](uint32_t key, uint32_t pos) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const uint32_t v = (key >> (8 * k)) & 0xFFu;
+        if (((tie >> k) & 1u) && cnt[0][k][v] == top_n[k]) atomicMax(&lst[k][v], pos);
+      }
+    });
+    __syncthreads();
+    if (tid < 3 && ((tie >> tid) & 1u)) best[tid] = ~0ull;
+    __syncthreads();
+    for (int i = tid; i < 3 * 256; i += kRangeBlock) {
+      const int k = i >> 8, v = i & 255;
+      if (((tie >> k) & 1u) && cnt[0][k][v] == top_n[k])
+        atomicMin(&best[k], ((unsigned long long)lst[k][v] << 8) | (unsigned)v);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    uint32_t win[3];
+    for (int k = 0; k < 3; ++k) win[k] = best[k] != ~0ull ? (uint32_t)(best[k] & 0xFFu) : 0u;  // none: m_max* = 0
+    uint16_t* o = a.out + (int64_t)f * 6;  // hpp:190-195: float constants promoted to double
+    o[0] = (uint16_t)((double)win[0] * (double)1.4f);
+    o[1] = 15;
+    o[2] = (uint16_t)((double)win[1] * (double)0.39f);
+    o[3] = 30;
+    o[4] = (uint16_t)((double)win[2] * (double)0.39f);
+    o[5] = 30;
+  }
+}
+
 }  // namespace
 
 // The 2:1 row kernel when the maps, layout and alignment allow (see
@@ -683,6 +867,37 @@ int launch_preview(const PreviewArgs& pa, const TrikHsvTargetSums* sums, int sum
 
 int launch_auto_range(const AutoRangeArgs& a, hipStream_t s) {
   if (a.n_frames <= 0) return hipSuccess;
+  // 16-byte aligned batches: the chunked two-pass kernel
+  const bool yuyv = a.layout == TRIK_HSV_LAYOUT_YUYV;
+  if ((yuyv || a.layout == TRIK_HSV_LAYOUT_OV7670) && (reinterpret_cast<uintptr_t>(a.frames) % 16) == 0 &&
+      (a.n_frames <= 1 || a.frame_stride % 16 == 0) && a.line_length % 16 == 0) {
+    const int pxc = yuyv ? 8 : 16;
+    AutoVecGeom g;
+    g.c0 = a.c_lo + 1 > 0 ? a.c_lo + 1 : 0;
+    g.c1 = a.c_hi < a.width ? a.c_hi : a.width;
+    g.r0 = a.r_lo + 1 > 0 ? a.r_lo + 1 : 0;
+    const int r1 = a.r_hi < a.height ? a.r_hi : a.height;
+    const int zw = g.c1 - g.c0, zh = r1 - g.r0;
+    int cpr = 0;
+    if (zw > 0 && zh > 0) {
+      g.k0 = g.c0 / pxc;
+      cpr = (g.c1 - 1) / pxc + 1 - g.k0;
+    } else {
+      g.k0 = 0;
+    }
+    // (the zone's last chunk must lie in its row)
+    if ((int64_t)16 * (g.k0 + cpr) <= a.line_length) {
+      g.per_row = make_div((uint32_t)(cpr > 0 ? cpr : 1));
+      g.total = (uint32_t)(cpr > 0 ? (int64_t)cpr * zh : 0);
+      if (yuyv)
+        hipLaunchKernelGGL(auto_range_vec_kernel<TRIK_HSV_LAYOUT_YUYV>, dim3((unsigned)a.n_frames), dim3(kRangeBlock), 0,
+                           s, a, g);
+      else
+        hipLaunchKernelGGL(auto_range_vec_kernel<TRIK_HSV_LAYOUT_OV7670>, dim3((unsigned)a.n_frames),
+                           dim3(kRangeBlock), 0, s, a, g);
+      return hipGetLastError();
+    }
+  }
   // one workgroup per frame; a few frames (process() takes one) get 1024
   // lanes each: the pass over the zone is a latency-bound chain per lane, 4x
   // shorter
