@@ -203,6 +203,12 @@ __device__ __forceinline__ void store_record(uint64_t m, uint32_t wa, u32x4 w, u
       : "memory", "scc");
 }
 
+// one 16-byte streaming (nontemporal) load
+__device__ __forceinline__ uint4 ld_nt16(const uint8_t* p) {
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // v if this lane's bit of wave mask m is set, else 0 (one v_cndmask; a
 // v_addc shift-in chain needs a wait state after every op on gfx950)
 __device__ __forceinline__ uint32_t lane_bit(uint64_t m, uint32_t v) {
@@ -214,6 +220,10 @@ __device__ __forceinline__ uint32_t spread4(uint32_t m) { return (m * 0x00204081
 
 // chroma index U | V << 8 of a YUYV word (b0=Y0, b1=U, b2=Y1, b3=V)
 __device__ __forceinline__ uint32_t chroma_of(uint32_t w) { return __builtin_amdgcn_perm(w, w, 0x0C0C0301u); }
+// the same shifted left by 8 (U << 8 | V << 16): the hot loop's run-descriptor
+// address 2c is then one right shift (v_lshrrev: half the issue cost of the
+// v_lshlrev that 2c needs; C4 -1 %, scripts/ab/r05j.py)
+__device__ __forceinline__ uint32_t chroma_of8(uint32_t w) { return __builtin_amdgcn_perm(w, w, 0x0C03010Cu); }
 
 // The exact mask (bit t = range t) of pixel PIX of YUYV word w: the stripe
 // kernel's arithmetic (trik_hsv_stripe_px.h: WSEQ:181-249 via v_dot4, the
@@ -657,8 +667,8 @@ __device__ __forceinline__ void load_chunk(const uint8_t* p, const uint8_t* pb, 
     w[0] = va.x; w[1] = va.y; w[2] = va.z; w[3] = va.w;
     w[4] = vb.x; w[5] = vb.y; w[6] = vb.z; w[7] = vb.w;
   } else {
-    const uint4 vy = *reinterpret_cast<const uint4*>(p);
-    const uint4 vc = *reinterpret_cast<const uint4*>(p + plane);
+    const uint4 vy = ld_nt16(p);  // (nontemporal: 1 % faster, scripts/ab/r05l_c7.py)
+    const uint4 vc = ld_nt16(p + plane);
     const uint32_t yy[4] = {vy.x, vy.y, vy.z, vy.w}, cc[4] = {vc.x, vc.y, vc.z, vc.w};
     // OSEQ:369-373: U = odd chroma byte, V = even chroma byte
 #pragma unroll
@@ -931,12 +941,12 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
         uint32_t c[CW], d[CW], cut[CW], pr[CW], e[2 * CW];
         u32x2 mm[CW];
 #pragma unroll
-        for (int i = 0; i < CW; ++i) c[i] = chroma_of(cw[i]);
+        for (int i = 0; i < CW; ++i) c[i] = chroma_of8(cw[i]);
 #pragma unroll
         for (int i = 0; i < CW; ++i) {
-          d[i] = ld16(kLdsRuns + 2u * c[i]);
+          d[i] = ld16(kLdsRuns + (c[i] >> 7));
           // the block word: the pair's palette offset | the cut << 8
-          cut[i] = ld16(kLdsBlocks + ((c[i] >> 3) & 0x1FFEu));
+          cut[i] = ld16(kLdsBlocks + ((c[i] >> 11) & 0x1FFEu));
           pr[i] = cut[i] & 0xFFu;
         }
 #pragma unroll
@@ -1244,8 +1254,8 @@ __global__ __launch_bounds__(kMaxBlock) void blob_chroma_meta_kernel(BlobArgs a,
   };
   Item cur = item_at(base, Item{a.frames, 0u, 0u, 0u, false});
   uint4 by[2], bc[2];
-  by[0] = *reinterpret_cast<const uint4*>(cur.p);
-  bc[0] = *reinterpret_cast<const uint4*>(cur.p + plane);
+  by[0] = ld_nt16(cur.p);
+  bc[0] = ld_nt16(cur.p + plane);
   for (;;) {
     const uint64_t vm = __builtin_amdgcn_ballot_w64(cur.valid);
     const uint32_t nb = base + stride;
@@ -1255,8 +1265,10 @@ __global__ __launch_bounds__(kMaxBlock) void blob_chroma_meta_kernel(BlobArgs a,
     for (int r = 0; r < 4; ++r) {
       // the next row: this item's r + 1, or the next item's row 0
       const uint8_t* np = r < 3 ? cur.p + (r + 1) * ll : nxt.p;
-      by[(r + 1) & 1] = *reinterpret_cast<const uint4*>(np);
-      bc[(r + 1) & 1] = *reinterpret_cast<const uint4*>(np + plane);
+      // streaming loads (nontemporal: 9 % faster on scenes than plain loads,
+      // scripts/ab/r05k_blob.py)
+      by[(r + 1) & 1] = ld_nt16(np);
+      bc[(r + 1) & 1] = ld_nt16(np + plane);
       const uint4 vy = by[r & 1], vc = bc[r & 1];
       const uint32_t yy[4] = {vy.x, vy.y, vy.z, vy.w}, cc[4] = {vc.x, vc.y, vc.z, vc.w};
       // the row's 8 words in two halves of 4 (registers: the next row's
@@ -1269,9 +1281,9 @@ __global__ __launch_bounds__(kMaxBlock) void blob_chroma_meta_kernel(BlobArgs a,
         for (int k = 0; k < 2; ++k) stripe_px::ov7670_words(yy[2 * hf + k], cc[2 * hf + k], w[2 * k], w[2 * k + 1]);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const uint32_t c = chroma_of(w[i]);
-          d[i] = ld16(kLdsRuns + 2u * c);
-          cut[i] = ld16(kLdsBlocks + ((c >> 3) & 0x1FFEu));
+          const uint32_t c = chroma_of8(w[i]);
+          d[i] = ld16(kLdsRuns + (c >> 7));
+          cut[i] = ld16(kLdsBlocks + ((c >> 11) & 0x1FFEu));
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) mm[i] = ld64(kLdsPairs + (cut[i] & 0xFFu));

@@ -102,8 +102,12 @@ __device__ __forceinline__ int line_rows(const uint8_t* yp, int64_t cofs, int64_
     uint2 y[4], c[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      y[i] = *reinterpret_cast<const uint2*>(p + i * step);
-      c[i] = *reinterpret_cast<const uint2*>(p + i * step + cofs);
+      // streaming loads (nontemporal: 8 % faster than plain, scripts/ab/r05l_line.py)
+      typedef unsigned int v2 __attribute__((ext_vector_type(2)));
+      const v2 ty = __builtin_nontemporal_load(reinterpret_cast<const v2*>(p + i * step));
+      const v2 tc = __builtin_nontemporal_load(reinterpret_cast<const v2*>(p + i * step + cofs));
+      y[i] = make_uint2(ty.x, ty.y);
+      c[i] = make_uint2(tc.x, tc.y);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
