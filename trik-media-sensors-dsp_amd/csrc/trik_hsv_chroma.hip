@@ -64,7 +64,7 @@ constexpr int kQueueCap = 128;  // blob kernel, entries per wave: < 64 waiting +
 // LDS image leaves; a step starts with < 64 records queued.
 constexpr int kHotLanes = 960;
 // the hot kernel's workgroup: 16 waves (4 per SIMD) whatever the tile's
-// lane count (<= kHotLanes: 15 wave-sized units at VGA); the waves pull the
+// lane count (<= kHotLanes: 10 wave-sized units at VGA); the waves pull the
 // units, so one more wave than units per tile costs nothing and fills the
 // fourth SIMD
 constexpr int kHotWaves = 16;
@@ -1377,9 +1377,15 @@ bool chroma_geometry(const KernelArgs& a, ChromaGeom& g) {
   const int64_t need = 16;  // vector loads
   if ((reinterpret_cast<uintptr_t>(a.frames) % need) || (a.frame_stride % need) || (a.line_length % need))
     return false;
-  int k = kHotLanes / cpr;
-  for (int kk = k; kk * 8 >= k * 7; --kk)
-    if ((kk * cpr) % 64 == 0) { k = kk; break; }
+  // 640 lanes when that makes whole waves: fewer, longer units per frame (the
+  // per-unit epilogue over more steps; VGA: 10 units of 30 steps instead of
+  // 15 of 20 -- C3 -0.3 %, scenes -1 %, scripts/ab/r05n_k.py)
+  int k = 640 / cpr;
+  if (k == 0 || (k * cpr) % 64 != 0) {
+    k = kHotLanes / cpr;
+    for (int kk = k; kk * 8 >= k * 7; --kk)
+      if ((kk * cpr) % 64 == 0) { k = kk; break; }
+  }
   g.cpr = cpr;
   g.k = k;
   g.dy = split && !wide ? k : 0;
