@@ -512,7 +512,7 @@ int32_t trik_hsv_batch_sums(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvFra
 #define TRIK_HSV_HOT_GENERIC 3
 #define TRIK_HSV_HOT_MIXED 4 /* trik_hsv_last_hot_kernel: the call's range groups ran different kernels */
 #define TRIK_HSV_CHROMA_MIN_PIXELS (32 * 640 * 480)
-#define TRIK_HSV_CHROMA_MAX_SHARE 0.25
+#define TRIK_HSV_CHROMA_MAX_SHARE 0.27 /* the measured crossover (profiles/r05/r05p_adversarial_4096.txt) */
 int32_t trik_hsv_set_hot_kernel(TRIK_VIDTRANSCODE_CV_Handle handle, int32_t kind);
 /* The chroma-run kernel's expected exact-path word share (uniform input) for
  * the handle's current batched-sums range set (the maximum over its groups of
