@@ -223,11 +223,8 @@ def load_traffic(path, bytes_per_launch):
         return None, f"none: {rel} was measured at another size"
     if pmc.get("source_digest") != source_digest():
         return None, f"none: {rel} was measured on other sources ({pmc.get('source_digest')})"
-    cal = pmc.get("hbm_read_bytes_per_launch_calibrated")
     return pmc.get("hbm_read_bytes_per_launch"), (f"committed PMC pass, {rel} (FETCH_SIZE x 2, "
-                                                  f"{pmc.get('measured', 'rocprofv3 --pmc')}; same sources)"
-                                                  + (f"; {cal} B after the access-pattern calibration "
-                                                     f"({pmc.get('calibration')})" if cal else ""))
+                                                  f"{pmc.get('measured', 'rocprofv3 --pmc')}; same sources)")
 
 
 def main():

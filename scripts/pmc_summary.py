@@ -5,13 +5,12 @@ usage: python scripts/pmc_summary.py PMC_DIR KERNEL_SUBSTRING BYTES_PER_LAUNCH [
 Averages every counter over the kernel's dispatches, then derives
   hbm_read_bytes_per_launch = FETCH_SIZE[KB] * 1024 * 2
 (MI355X_MICROARCH.md, HBM section: on gfx950 FETCH_SIZE reports exactly half
-the bytes of a wide coalesced streaming read, so it is doubled), and
-  hbm_read_bytes_per_launch_calibrated = that / FETCH_CALIB
-where FETCH_CALIB (1.024) is the same figure over the known byte count of a
-pure read stream in the chroma kernel's access pattern (two nontemporal 16-B
-loads per 32-B lane chunk, 256 x 1024 lanes; scripts/ubench/fetch_calib.hip,
-profiles/r05/fetch_calib/): the x2 rule over-counts that pattern by 2.4 %
-(RDREQ x 128 B, but ~2.4 % of the pattern's requests are 64-B halves).
+the bytes of a wide coalesced streaming read, so it is doubled).  Calibrated
+on a known byte count in the chroma kernel's own access pattern
+(scripts/ubench/fetch_calib.hip calib_rows, profiles/r05/fetch_calib/): the
+doubled figure is 1.0000 x the bytes read there (a lane-interleaved pattern,
+two 16-B loads per 32-B lane chunk, reads 1.024 x: some of its requests are
+64-B halves), so for this kernel the doubled figure is the traffic.
 BYTES_PER_LAUNCH is the algorithmic input bytes of one launch (2 B/pixel),
 written alongside so bench.py only uses the traffic figure for the same size.
 """
@@ -21,12 +20,6 @@ import glob
 import json
 import os
 import sys
-
-# FETCH_SIZE(KB)*1024*2 / bytes read, for a 2,516,582,400-B stream in the
-# chroma kernel's pattern (profiles/r05/fetch_calib/pass1_counter_collection.csv:
-# the warm calib_stream / calib_stage_stream dispatches 4-5, 9-11 average
-# 1,258,225 KB -> 2.5769e9 B; the cold first dispatch reads 0.4 % more)
-FETCH_CALIB = 1.024
 
 
 def main():
@@ -55,11 +48,9 @@ def main():
         hbm = avg["FETCH_SIZE"] * 1024 * 2
         res["hbm_read_bytes_per_launch"] = int(hbm)
         res["hbm_read_over_algorithmic"] = round(hbm / alg, 4)
-        res["correction"] = "FETCH_SIZE(KB)*1024*2 (gfx950 reports half of 16-B/lane streaming reads)"
-        res["hbm_read_bytes_per_launch_calibrated"] = int(hbm / FETCH_CALIB)
-        res["hbm_read_over_algorithmic_calibrated"] = round(hbm / FETCH_CALIB / alg, 4)
-        res["calibration"] = (f"/ {FETCH_CALIB}: FETCH_SIZE*2 over the known bytes of a pure read stream in this "
-                              "access pattern (scripts/ubench/fetch_calib.hip, profiles/r05/fetch_calib/)")
+        res["correction"] = ("FETCH_SIZE(KB)*1024*2 (gfx950 reports half of 16-B/lane streaming reads; 1.0000 x "
+                             "the known bytes of a stream in the chroma kernel's own pattern, "
+                             "profiles/r05/fetch_calib/)")
     px = alg / 2
     if "SQ_INSTS_VALU" in avg and "SQ_WAVES" in avg:
         res["valu_instr_per_pixel_per_lane"] = round(avg["SQ_INSTS_VALU"] * 64 / px, 2)

@@ -627,6 +627,7 @@ struct ChromaGeom {
   // ceil(2^20 / cpr), exact for lt < 1024 and cpr < 1024
   FastDiv fd_units, fd_tiles;
   uint32_t cpr_inv;
+  int32_t tail_ok;  // the past-the-end loads fit inside the ChromaTables block
   int32_t units;  // wave-sized units per tile: ceil(k * cpr / 64) <= kHotWaves
 };
 
@@ -1034,10 +1035,14 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
       };
       // rows of step s + 1 loaded while step s is processed (a third buffer,
       // two steps ahead, measured no faster: the kernel is VALU-bound)
-      // (the load past the tile's last step re-reads its last rows: an
-      // unconditional load keeps the step's wait at "this step's data"; a
-      // branch around it makes the compiler wait for every load in flight)
+      // (the load past the tile's last step is unconditional: that keeps the
+      // step's wait at "this step's data", where a branch around it makes the
+      // compiler wait for every load in flight.  It reads the start of the
+      // ChromaTables block, L2-resident, when the lanes' offsets fit inside
+      // it (tail_ok) -- re-reading the tile's last rows instead cost 2.2 %
+      // extra HBM reads, scripts/ab/r05s_tail.py)
       const uint8_t* rb = tbase;
+      const uint8_t* const tail = reinterpret_cast<const uint8_t*>(ct);
       auto ld = [&](int s, uint32_t (&w)[CW]) {
         if (FULL) load_chunk<LAYOUT>(rb + voff, rb + hb + voff, plane, w);
         else
@@ -1047,11 +1052,11 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
       uint32_t wa[CW], wb[CW];
       ld(0, wa);
       for (int s = 0; s < steps; s += 2) {
-        if (FULL && s + 1 < steps) rb += rowstep;
+        if (FULL) rb = s + 1 < steps ? rb + rowstep : (g.tail_ok ? tail : rb);
         ld(s + 1, wb);
         step(wa, s);
         if (s + 1 >= steps) break;
-        if (FULL && s + 2 < steps) rb += rowstep;
+        if (FULL) rb = s + 2 < steps ? rb + rowstep : (g.tail_ok ? tail : rb);
         ld(s + 2, wa);
         step(wb, s + 1);
       }
@@ -1406,6 +1411,7 @@ bool chroma_geometry(const KernelArgs& a, ChromaGeom& g) {
   int r = 65535 / (2 * span);
   g.flush_rounds = r > 127 ? 127 : r;
   g.units = (g.k * g.cpr + 63) / 64;
+  g.tail_ok = (int64_t)(g.k + g.dy) * a.line_length + 2LL * g.dx + 16 <= (int64_t)sizeof(ChromaTables);
   g.fd_units = make_div((uint32_t)g.units);
   g.fd_tiles = make_div((uint32_t)g.tiles_per_frame);
   g.cpr_inv = (uint32_t)(((1u << 20) + (uint32_t)cpr - 1) / (uint32_t)cpr);
