@@ -1118,7 +1118,11 @@ int32_t ensure_blob_scratch(TrikCvHandle* h, int n, int w, int hgt, hipStream_t 
     h->blob_users.wait_all();
   HIP_TRY(h->blob_users.order_after(s));
   int32_t r = grow(h->d_meta, h->d_meta_cap, nn * (bw * bh > 0 ? bw * bh : 1));
+  // the clusterer's own statistics: zero when allocated, and every clusterer
+  // launch leaves the labels it used zero again (blob_ccl_kernel)
+  const bool fresh_stats = nn * 3 * ml * sizeof(int32_t) > h->d_blob_stats_cap;
   if (!r) r = grow(h->d_blob_stats, h->d_blob_stats_cap, nn * 3 * ml * sizeof(int32_t));
+  if (!r && fresh_stats) HIP_TRY(hipMemsetAsync(h->d_blob_stats, 0, h->d_blob_stats_cap, s));
   if (!r) r = grow(h->d_blob_top, h->d_blob_top_cap, nn * 24 * sizeof(int32_t));
   if (!r) r = grow(h->d_blob_targets, h->d_blob_targets_cap, nn * 8 * sizeof(TrikHsvTarget));
   return r;

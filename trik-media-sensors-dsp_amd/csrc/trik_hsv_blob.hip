@@ -518,6 +518,15 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
     }
   }
   if (lane == 0 && a.n_labels) a.n_labels[f] = n;
+  // leave the own statistics zero for the next launch: this frame used labels
+  // 1 .. n - 1 only (every read of them above has returned: lane 0's last
+  // reads fed the stores before this loop), so zeroing those restores the
+  // all-zero buffer launch_blob relies on -- no memset of all max_labels
+  // slots per frame (157 MB for 4096 VGA frames) before every batch
+  for (int k = lane; k < n; k += 64) {
+    if (packed) own64[k] = 0ull;
+    else own[3 * k] = own[3 * k + 1] = own[3 * k + 2] = 0;
+  }
 }
 
 template <bool LDSMAP>
@@ -564,10 +573,9 @@ int launch_blob(const BlobArgs& a, hipStream_t s) {
       b.pack_sy = bn + bx;
     }
   }
-  // own statistics start at zero (at the front of stats)
-  const size_t own_bytes = (b.pack_sx ? sizeof(uint64_t) : 3 * sizeof(int32_t)) * (size_t)a.max_labels * (size_t)a.n_frames;
-  hipError_t z = hipMemsetAsync(a.stats, 0, own_bytes, s);
-  if (z != hipSuccess) return z;
+  // own statistics start at zero (at the front of stats): the buffer is
+  // zeroed when it is allocated (ensure_blob_scratch) and every clusterer
+  // launch zeroes the labels it used before it ends
   const int64_t total = (int64_t)a.n_frames * bw * bh;
   if (total >= (1ll << 31) || !a.tables) return hipErrorInvalidValue;
   {
