@@ -240,3 +240,29 @@ def test_blob_batch_large_from_l2(hsv, oracle_mod):
             _check(oracle_mod, res, i, fr, w, h, ll, RED, cases[i])
     finally:
         det.close()
+
+
+def test_blob_stats_clean_across_geometries(hsv, oracle_mod):
+    """One handle, batches of changing geometry: the clusterer's statistics
+    buffer is not cleared per batch -- it is zeroed when allocated and every
+    clusterer wave zeroes the labels it used before it ends -- so each batch
+    here runs on what the previous one (another layout, packed or three-int
+    statistics) left behind.  1024 x 1024 takes the unpacked statistics
+    (size, sum x, sum y do not fit 63 bits together)."""
+    import torch
+
+    seq = [((640, 480, 640), [("meta", 71, 0.5), ("meta", 72, 0.75)]),
+           ((1024, 1024, 1024), [("meta", 73, 0.5), ("scene", 74, 0.02)]),
+           ((320, 240, 352), [("scene", 75, 0.03), ("meta", 76, 0.3)]),
+           ((640, 480, 640), [("meta", 77, 0.75), ("meta", 78, 0.1)]),
+           ((1024, 1024, 1024), [("meta", 79, 0.3)])]
+    det = hsv.Detector()
+    try:
+        for (w, h, ll), cases in seq:
+            frames = _frames(oracle_mod, w, h, ll, cases)
+            dev = torch.from_numpy(np.concatenate(frames)).cuda()
+            res = det.blob_batch(dev, w, h, ll, RED, meta=True, labels=True)
+            for i, fr in enumerate(frames):
+                _check(oracle_mod, res, i, fr, w, h, ll, RED, ((w, h), cases[i]))
+    finally:
+        det.close()
