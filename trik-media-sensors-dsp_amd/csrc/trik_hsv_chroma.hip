@@ -1411,7 +1411,10 @@ bool chroma_geometry(const KernelArgs& a, ChromaGeom& g) {
   int r = 65535 / (2 * span);
   g.flush_rounds = r > 127 ? 127 : r;
   g.units = (g.k * g.cpr + 63) / 64;
-  g.tail_ok = (int64_t)(g.k + g.dy) * a.line_length + 2LL * g.dx + 16 <= (int64_t)sizeof(ChromaTables);
+  // the past-the-end loads may read the ChromaTables block instead (YUYV: a
+  // lane's two loads lie within (k + dy) rows + 2 dx bytes of the base; the
+  // ov7670 layout's second load is a whole luma plane further: never)
+  g.tail_ok = split && (int64_t)(g.k + g.dy) * a.line_length + 2LL * g.dx + 16 <= (int64_t)sizeof(ChromaTables);
   g.fd_units = make_div((uint32_t)g.units);
   g.fd_tiles = make_div((uint32_t)g.tiles_per_frame);
   g.cpr_inv = (uint32_t)(((1u << 20) + (uint32_t)cpr - 1) / (uint32_t)cpr);
