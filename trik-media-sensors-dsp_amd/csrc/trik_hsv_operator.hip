@@ -166,7 +166,7 @@ void preview_gather_kernel(PreviewArgs a, PreviewGeom g) {
       uint8_t* row = a.previews + (int64_t)ff[u] * a.preview_stride + (int64_t)rr[u] * a.out_ll;
       const int b0 = 4 * (int)qq[u];
       if (a.aligned4 && b0 + 4 <= a.out_ll) {
-        *reinterpret_cast<uint32_t*>(row + b0) = out[u];
+        __builtin_nontemporal_store(out[u], reinterpret_cast<uint32_t*>(row + b0));  // (as the 2:1 kernel's)
       } else {
         for (int k = 0; k < 4 && b0 + k < a.out_ll; ++k) row[b0 + k] = (uint8_t)(out[u] >> (8 * k));
       }
@@ -215,6 +215,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8)))
 void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
   using namespace stripe_px;
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
   constexpr bool YUYV = LAYOUT == TRIK_HSV_LAYOUT_YUYV;
   constexpr int PX = 8;  // output pixels per unit
   // (META: the multi-blob preview's metapixel flags as the detection, a
@@ -338,12 +339,16 @@ void preview_rows2_kernel(PreviewArgs a, PreviewRowsGeom g) {
       if (ff[u] < nf) {
         uint8_t* dst = a.previews + (uint64_t)ff[u] * (uint32_t)a.preview_stride +
                        (__umul24(rr[u], (uint32_t)a.out_ll) + 2u * PX * qq[u]);
+        // nontemporal stores: the preview is written once and not read back
+        // here (630 MB per 4096 VGA frames; plain stores left back-to-back
+        // batches waiting on the write-backs: 0.51 -> 0.45-0.47 ms,
+        // scripts/ab/r05zc_preview_nt.py)
 #pragma unroll
         for (int h = 0; h < PX / 4; ++h) {
-          uint2 o;
+          u32x2 o;
           o.x = v[4 * h] | (v[4 * h + 1] << 16);
           o.y = v[4 * h + 2] | (v[4 * h + 3] << 16);
-          *reinterpret_cast<uint2*>(dst + 8 * h) = o;
+          __builtin_nontemporal_store(o, reinterpret_cast<u32x2*>(dst + 8 * h));
         }
       }
     }
