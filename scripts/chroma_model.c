@@ -91,8 +91,10 @@ static uint32_t desc_cut(int c, uint32_t k, uint32_t A) {
 
 // block b's 16 chromas under a block layout
 static int LAYOUT = 0;
+static int BS = 16;  // chromas per block (16: the kernel's; 8: a finer variant)
 static FILE* dump = NULL;  // 0: 16 along U (the kernel's), 1: 16 along V, 2: 4 x 4
 static int chroma_in_block(int b, int i) {
+  if (BS == 8) return ((b >> 5) << 8) | ((b & 31) << 3) | i;     // V = b >> 5, U = 8 (b & 31) + i
   if (LAYOUT == 0) return ((b >> 4) << 8) | ((b & 15) << 4) | i;  // V = b >> 4, U = 16 (b & 15) + i
   if (LAYOUT == 1) return (((b & 15) * 16 + i) << 8) | (b >> 4);  // U = b >> 4, V = 16 (b & 15) + i
   // 4 x 4: b = (V >> 2) << 6 | (U >> 2)
@@ -106,15 +108,15 @@ typedef struct {
 
 static uint64_t block_best(int b, const int* allowed /* [256] or NULL */) {
   int cs[16];
-  for (int i = 0; i < 16; ++i) cs[i] = chroma_in_block(b, i);
+  for (int i = 0; i < BS; ++i) cs[i] = chroma_in_block(b, i);
   uint32_t cuts[17];
   int nc = 0;
   cuts[nc++] = 0;
-  for (int i = 0; i < 16; ++i)
+  for (int i = 0; i < BS; ++i)
     if (FZ[cs[i]] != 0 && FZ[cs[i]] <= 255) cuts[nc++] = (uint32_t)FZ[cs[i]];
   uint32_t present = 1;
   if (!allowed)
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < BS; ++i) {
       const uint32_t a = SF[cs[i]], d = SD[cs[i]];
       if (a & 3u) present |= 1u << ((a >> 4) & 15u);
       if ((a & 3u) == 2u) present |= 1u << ((a >> 8) & 15u);
@@ -127,7 +129,7 @@ static uint64_t block_best(int b, const int* allowed /* [256] or NULL */) {
     if (!take) continue;
     for (int j = 0; j < nc; ++j) {
       uint64_t cost = 0;
-      for (int i = 0; i < 16; ++i) cost += cost_words(desc_cut(cs[i], k, cuts[j]));
+      for (int i = 0; i < BS; ++i) cost += cost_words(desc_cut(cs[i], k, cuts[j]));
       const uint64_t key = (cost << 17) | ((uint64_t)k << 9) | cuts[j];
       if (key < best) best = key;
     }
@@ -137,10 +139,11 @@ static uint64_t block_best(int b, const int* allowed /* [256] or NULL */) {
 
 static double model(int layout, int palette, const char* label, int verbose) {
   LAYOUT = layout;
-  static uint64_t best[4096];
+  static uint64_t best[8192];
   static int hist[256];
+  const int nb = NC / BS;
   memset(hist, 0, sizeof hist);
-  for (int b = 0; b < 4096; ++b) {
+  for (int b = 0; b < nb; ++b) {
     best[b] = block_best(b, NULL);
     hist[(best[b] >> 9) & 255]++;
   }
@@ -152,11 +155,11 @@ static double model(int layout, int palette, const char* label, int verbose) {
   }
   uint64_t total = 0, exc_c = 0, win_c = 0, exc_cost = 0, win_cost = 0, pix = 0;
   uint64_t hL[257] = {0};
-  for (int b = 0; b < 4096; ++b) {
+  for (int b = 0; b < nb; ++b) {
     uint64_t key = best[b];
     if (!allowed[(key >> 9) & 255]) key = block_best(b, allowed);
     const uint32_t k = (uint32_t)(key >> 9) & 255u, A = (uint32_t)key & 511u;
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < BS; ++i) {
       const int c = chroma_in_block(b, i);
       const uint32_t d = desc_cut(c, k, A);
       const uint32_t cw = cost_words(d);
@@ -226,5 +229,9 @@ int main(int argc, char** argv) {
   model(0, 256, "16 along U, pal 256", 0);
   model(1, 32, "16 along V, pal 32", 0);
   model(2, 32, "4 x 4, pal 32", 0);
+  BS = 8;
+  model(0, 32, "8 along U, pal 32", 0);
+  model(0, 64, "8 along U, pal 64", 0);
+  BS = 16;
   return 0;
 }
