@@ -254,3 +254,28 @@ def test_auto_share_guard(torch_dev, hsv, oracle_mod):
             assert np.array_equal(sums.cpu().numpy(), want)
     finally:
         d.close()
+
+
+@pytest.mark.parametrize("ll", [1280, 1296, 65536])
+def test_chroma_tail_loads_either_side_of_the_bound(torch_dev, hsv, detector, oracle_mod, chroma, ll):
+    """The unconditional load past a tile's last step reads the ChromaTables
+    block when a lane's two loads fit inside it ((k + dy) rows + 16 bytes;
+    chroma_geometry's tail_ok), else the tile's last rows again: VGA YUYV
+    with the row bytes, a little padding, and 64 KiB lines (16 rows of those
+    do not fit).  Both the separate-kernel path and the fused step, against
+    the oracle."""
+    torch = torch_dev
+    w, h, n = 640, 480, 3
+    fb = h * ll
+    host = oracle_mod.synth(n, w, h, ll, LAYOUT_YUYV, 0, 0x7A1C, first_frame=7)
+    dev = _to_dev(torch, host)
+    want_s, want_t = oracle_mod.batch(host, fb, n, w, h, ll, LAYOUT_YUYV, BENCH_RANGES, n_threads=8)
+    sums, tg = detector.process_batch(dev, w, h, ll, LAYOUT_YUYV, BENCH_RANGES)
+    assert detector.last_hot_kernel() == hsv.HOT_CHROMA
+    assert np.array_equal(sums.cpu().numpy(), want_s), ll
+    assert np.array_equal(tg[:, :, :3].cpu().numpy(), want_t), ll
+    s2, t2, tot = detector.process_batch_totals(dev, w, h, ll, LAYOUT_YUYV, BENCH_RANGES)
+    torch.cuda.synchronize()
+    assert np.array_equal(s2.cpu().numpy(), want_s), ll
+    assert np.array_equal(t2[:, :, :3].cpu().numpy(), want_t), ll
+    assert np.array_equal(tot.cpu().numpy(), want_s.sum(0)), ll
