@@ -89,6 +89,10 @@ def parse():
                     help="N > 1 over nccl: the totals' all-reduce through the library's own RCCL communicator "
                          "(comm: trik_hsv_comm_all_reduce_totals, double-buffered on a second stream) or "
                          "torch.distributed's (torch: in series on the step's stream)")
+    ap.add_argument("--reserve-cus", type=int, default=2,
+                    help="with the library's communicator: CUs the hot kernel leaves free so that the all-reduce "
+                         "kernel on the second stream runs beside the next step's kernel (trik_hsv_set_reserved_cus; "
+                         "the hot kernel takes one 160-KiB-LDS workgroup per CU)")
     ap.add_argument("--comm-self", action="store_true",
                     help="at N = 1 too: a library communicator of one rank, the same double-buffered "
                          "all-reduce (exercises the N > 1 step's code path on one GPU)")
@@ -288,13 +292,22 @@ def main():
             dist.broadcast_object_list(uid, src=0)
         comm = trik_hsv.Comm(world, rank, uid[0])
     comm_stream = torch.cuda.Stream(device=dev) if comm is not None else None
+    if comm is not None and args.reserve_cus > 0:
+        det.set_reserved_cus(args.reserve_cus)
     kern_done = [torch.cuda.Event(), torch.cuda.Event()]
     red_done = [None, None]
     if comm is not None:
         collective = {"call": "trik_hsv_comm_all_reduce_totals (the library's RCCL communicator, C ABI)",
                       "ranks": world, "bytes": 24 * T,
                       "overlap": "double-buffered totals: step k's all-reduce on a second stream while step "
-                                 "k+1's kernel runs; step k+2 waits for it on the device"}
+                                 "k+1's kernel runs; step k+2 waits for it on the device",
+                      "reserved_cus": args.reserve_cus,
+                      "overlap_evidence": "the hot kernel holds one 160-KiB-LDS workgroup on every CU it is given; "
+                                          "a kernel on another stream runs beside it only on CUs left free "
+                                          "(profiles/r06/overlap_*: scripts/overlap_probe.py traces)",
+                      "tests": "one-rank comm (tests/test_gpu_multirank.py::test_bench_library_comm_one_rank); "
+                               "two ranks over nccl: test_bench_two_ranks_library_comm_nccl (runs where 2 GPUs "
+                               "are visible)"}
     elif world > 1 and backend == "nccl":
         collective = {"call": "torch.distributed.all_reduce (RCCL)", "ranks": world, "bytes": 24 * T,
                       "overlap": "none: in series after each step's kernel"}

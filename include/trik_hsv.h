@@ -512,7 +512,7 @@ int32_t trik_hsv_batch_sums(TRIK_VIDTRANSCODE_CV_Handle handle, const TrikHsvFra
 #define TRIK_HSV_HOT_GENERIC 3
 #define TRIK_HSV_HOT_MIXED 4 /* trik_hsv_last_hot_kernel: the call's range groups ran different kernels */
 #define TRIK_HSV_CHROMA_MIN_PIXELS (32 * 640 * 480)
-#define TRIK_HSV_CHROMA_MAX_SHARE 0.27 /* the measured crossover (DESIGN.md 4.6, profiles/r05/r05p_adversarial_4096.txt) */
+#define TRIK_HSV_CHROMA_MAX_SHARE 0.27 /* the measured crossover (DESIGN.md 4.5, profiles/r05/r05p_adversarial_4096.txt) */
 int32_t trik_hsv_set_hot_kernel(TRIK_VIDTRANSCODE_CV_Handle handle, int32_t kind);
 /* The chroma-run kernel's expected exact-path word share (uniform input) for
  * the handle's current batched-sums range set (the maximum over its groups of
@@ -534,6 +534,15 @@ int32_t trik_hsv_chroma_measured_share(TRIK_VIDTRANSCODE_CV_Handle handle, doubl
  * leaves the answer unchanged).  When the device chose (see above) this waits for
  * the builder's readback. */
 int32_t trik_hsv_last_hot_kernel(TRIK_VIDTRANSCODE_CV_Handle handle);
+/* CUs the chroma-run hot kernel leaves free (0 by default): its grid is one
+ * 160-KiB-LDS workgroup per CU the stream may use, so a kernel on another
+ * stream (the per-step all-reduce of the totals over RCCL, multi-GPU) waits
+ * for a CU to free up unless some stay free.  n CUs fewer: ~n/256 slower at
+ * MI355X's 256 CUs; results are identical.  0 <= n <= 32; returns the
+ * previous setting, or -1 for a NULL handle or an n out of range.  A stream
+ * created with a CU mask (hipExtStreamCreateWithCUMask) is sized to its mask
+ * where the runtime reports it. */
+int32_t trik_hsv_set_reserved_cus(TRIK_VIDTRANSCODE_CV_Handle handle, int32_t n);
 
 /* Epilogue only: sums_dev -> targets_dev for an n_frames x n_ranges grid. */
 int32_t trik_hsv_batch_targets(const TrikHsvFrameBatch* batch, int32_t n_ranges,

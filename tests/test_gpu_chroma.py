@@ -256,25 +256,44 @@ def test_auto_share_guard(torch_dev, hsv, oracle_mod):
         d.close()
 
 
-@pytest.mark.parametrize("ll", [1280, 1296, 65536])
-def test_chroma_tail_loads_either_side_of_the_bound(torch_dev, hsv, detector, oracle_mod, chroma, ll):
-    """The unconditional load past a tile's last step reads the ChromaTables
-    block when a lane's two loads fit inside it ((k + dy) rows + 16 bytes;
-    chroma_geometry's tail_ok), else the tile's last rows again: VGA YUYV
-    with the row bytes, a little padding, and 64 KiB lines (16 rows of those
-    do not fit).  Both the separate-kernel path and the fused step, against
-    the oracle."""
+# (layout, w, h, ll): where the past-the-end loads go.  YUYV spans (k + dy)
+# rows + 16 bytes of a tile base, ov7670 a luma plane + k rows: VGA YUYV at the
+# row bytes, with padding and with 64 KiB lines (1 MiB: larger than the
+# ChromaTables block the round-5 kernel read, inside the 4 MiB sink), YUYV
+# lines of 272 KiB (4.25 MiB: past the sink, so the tile's last rows are
+# re-read), ov7670 VGA (317 KB), ov7670 1280x720 (0.93 MB, larger than the
+# ChromaTables block: the geometry that faulted in round 5 would have been
+# of this kind), and ov7670 with 9 KiB lines (a 4.4 MB plane: re-read).
+TAIL_GEOMS = [
+    (LAYOUT_YUYV, 640, 480, 1280),
+    (LAYOUT_YUYV, 640, 480, 1296),
+    (LAYOUT_YUYV, 640, 480, 65536),
+    (LAYOUT_YUYV, 640, 480, 278528),
+    (LAYOUT_OV7670, 640, 480, 640),
+    (LAYOUT_OV7670, 1280, 720, 1280),
+    (LAYOUT_OV7670, 640, 480, 9216),
+]
+
+
+@pytest.mark.parametrize("layout,w,h,ll", TAIL_GEOMS)
+def test_chroma_tail_loads_either_side_of_the_sink(torch_dev, hsv, detector, oracle_mod, chroma, layout, w, h, ll):
+    """The unconditional load past a tile's last step reads the handle's
+    tail sink (KernelArgs::tail, 4 MiB) when every lane's two loads fit inside
+    it (chroma_tail_span), else the tile's last rows again: no load depends on
+    the address of another allocation.  Geometries on both sides of the sink
+    in both layouts (TAIL_GEOMS); the separate-kernel path and the fused step,
+    against the oracle."""
     torch = torch_dev
-    w, h, n = 640, 480, 3
-    fb = h * ll
-    host = oracle_mod.synth(n, w, h, ll, LAYOUT_YUYV, 0, 0x7A1C, first_frame=7)
+    n = 3
+    fb = oracle_mod.frame_bytes(w, h, ll, layout)
+    host = oracle_mod.synth(n, w, h, ll, layout, 0, 0x7A1C, first_frame=7)
     dev = _to_dev(torch, host)
-    want_s, want_t = oracle_mod.batch(host, fb, n, w, h, ll, LAYOUT_YUYV, BENCH_RANGES, n_threads=8)
-    sums, tg = detector.process_batch(dev, w, h, ll, LAYOUT_YUYV, BENCH_RANGES)
+    want_s, want_t = oracle_mod.batch(host, fb, n, w, h, ll, layout, BENCH_RANGES, n_threads=8)
+    sums, tg = detector.process_batch(dev, w, h, ll, layout, BENCH_RANGES)
     assert detector.last_hot_kernel() == hsv.HOT_CHROMA
     assert np.array_equal(sums.cpu().numpy(), want_s), ll
     assert np.array_equal(tg[:, :, :3].cpu().numpy(), want_t), ll
-    s2, t2, tot = detector.process_batch_totals(dev, w, h, ll, LAYOUT_YUYV, BENCH_RANGES)
+    s2, t2, tot = detector.process_batch_totals(dev, w, h, ll, layout, BENCH_RANGES)
     torch.cuda.synchronize()
     assert np.array_equal(s2.cpu().numpy(), want_s), ll
     assert np.array_equal(t2[:, :, :3].cpu().numpy(), want_t), ll

@@ -127,3 +127,32 @@ def test_bench_library_comm_one_rank():
     assert "double-buffered" in d["collective"]["overlap"]
     chk = d["totals_check"]
     assert chk["ok"] is True and chk["frames_reduced"] == 64 and all(p > 0 for p in chk["points"])
+
+
+def test_bench_two_ranks_library_comm_nccl():
+    """bench.py's multi-GPU collective as the driver runs it: two ranks, one
+    GPU each, over nccl (RCCL), the totals all-reduced by the library's own
+    communicator, double-buffered on a second stream -- buffer reuse two steps
+    apart, the red_done waits and the two buffers' equality across ranks are
+    all inside totals_check.  Needs two visible GPUs (the test box has one:
+    skipped there; the driver's 8-GPU SCALE run is the same code path)."""
+    import torch
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.pop("TRIK_BENCH_BACKEND", None)
+    env.pop("TRIK_BENCH_DEVICE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "3", "--frames", "64",
+           "--no-cpu-baseline", "--no-extras"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["ranks"] == 2 and d["backend"].startswith("nccl")
+    assert d["collective"]["call"].startswith("trik_hsv_comm_all_reduce_totals") and d["collective"]["ranks"] == 2
+    chk = d["totals_check"]
+    assert chk["ok"] is True and chk["frames_reduced"] == 128 and all(p > 0 for p in chk["points"])

@@ -127,11 +127,22 @@ def test_batch_auto_range(hsv, oracle_mod, w, h, ll, layout, kind):
                                    want["detect_val_tol"]], f
 
 
+def _auto_want(oracle_mod, host, fb, n, w, h, ll, layout):
+    out = []
+    for f in range(n):
+        _, want, _ = oracle_mod.run(host[f * fb:(f + 1) * fb], w, h, ll, layout, T0,
+                                    auto_detect=True, preview=False)
+        out.append([want["detect_hue"], want["detect_hue_tol"], want["detect_sat"],
+                     want["detect_sat_tol"], want["detect_val"], want["detect_val_tol"]])
+    return out
+
+
 @pytest.mark.parametrize("layout", [LAYOUT_YUYV, LAYOUT_OV7670])
 def test_batch_auto_range_large_batch(hsv, oracle_mod, layout):
-    """>= 512 frames take the two-pass kernel, fewer the one-pass kernel with
-    256 lanes per frame, <= 32 frames the one with 1024
-    (operator.hip:launch_auto_range): all three = the oracle, frame by frame."""
+    """16-byte aligned batches take the chunked two-pass kernel
+    (auto_range_vec_kernel) at every batch size: 520, 64 and 16 frames of the
+    same data agree with each other and with the oracle, frame by frame.
+    (The one-pass fallback kernels: test_batch_auto_range_fallback_kernels.)"""
     import torch
 
     w, h, n = 160, 120, 520
@@ -151,6 +162,96 @@ def test_batch_auto_range_large_batch(hsv, oracle_mod, layout):
         assert got[f].tolist() == [want["detect_hue"], want["detect_hue_tol"], want["detect_sat"],
                                    want["detect_sat_tol"], want["detect_val"],
                                    want["detect_val_tol"]], f
+
+
+# Batches launch_auto_range cannot give the chunked kernel (a frames pointer
+# 4 bytes past a 16-byte boundary, or a line length that is not a multiple of
+# 16): <= 32 frames run auto_range_kernel<1024>, more auto_range_kernel<256>.
+@pytest.mark.parametrize("w,h,ll,layout,n,offset", [
+    (640, 480, 1280, LAYOUT_YUYV, 6, 4),      # misaligned base, <1024>
+    (640, 480, 1280, LAYOUT_YUYV, 40, 4),     # misaligned base, <256>
+    (96, 72, 200, LAYOUT_YUYV, 8, 0),         # line length % 16 == 8, <1024>
+    (96, 72, 200, LAYOUT_YUYV, 48, 0),        # <256>
+    (320, 240, 324, LAYOUT_OV7670, 5, 0),     # ov7670, line length % 16 == 4, <1024>
+    (320, 240, 320, LAYOUT_OV7670, 36, 4),    # ov7670 misaligned base, <256>
+])
+def test_batch_auto_range_fallback_kernels(hsv, oracle_mod, w, h, ll, layout, n, offset):
+    import torch
+
+    fb = hsv.frame_bytes(w, h, ll, layout)
+    raw = torch.empty(n * fb + 16, dtype=torch.uint8, device="cuda")
+    dev = raw[offset:offset + n * fb]
+    assert dev.data_ptr() % 16 == offset
+    hsv.synth(dev, w, h, ll, layout, 1, SEED + 3, first_frame=11)
+    got = hsv.batch_auto_range(dev, w, h, ll, layout).cpu().numpy().astype(np.int64)
+    host = dev.cpu().numpy()
+    assert got.tolist() == _auto_want(oracle_mod, host, fb, n, w, h, ll, layout)
+
+
+def _zone_hsv(table, fr, w, h, ll):
+    """The strict central zone's per-pixel (H, S, V) of a YUYV frame in scan
+    order (cv_hsv_range_detector.hpp:88-108 bounds), from the oracle's table."""
+    px = fr[: h * ll].reshape(h, ll)[:, : 2 * w].reshape(h, w // 2, 4).astype(np.int64)
+    Y = np.stack([px[..., 0], px[..., 2]], -1).reshape(h, w)
+    U = np.repeat(px[..., 1], 2, axis=1)
+    V = np.repeat(px[..., 3], 2, axis=1)
+    step = h // 6
+    r0, r1, c0, c1 = h // 2 - step + 1, h // 2 + step, w // 2 - step + 1, w // 2 + step
+    e = table[(Y | (U << 8) | (V << 16))[r0:r1, c0:c1]].reshape(-1) & 0xFFFFFFFF
+    return [(e >> sh) & 0xFF for sh in (0, 8, 16)]
+
+
+def _tie_frame(w, h, ll, first):
+    """A YUYV frame whose central zone holds two colours with equal counts
+    (54 zone rows each, 8,586 pixels) and a third with fewer (51 rows): every
+    channel's maximum count is tied between A = (Y 100, U 90, V 200), HSV
+    (7, 230, 211), and B = (Y 60, U 200, V 90), HSV (158, 254, 196); the third
+    colour is grey (Y 120), HSV (85, 0, 120).  `first` ('A' or 'B') fills the
+    upper 54 zone rows: its last occurrence comes first, so the sequential
+    arg-max picks it in every channel."""
+    words = np.zeros((h, ll // 4, 4), np.uint8)
+    words[:, :, :] = (120, 128, 120, 128)
+    A, B = (100, 90, 100, 200), (60, 200, 60, 90)
+    step = h // 6
+    r0, c0, c1 = h // 2 - step + 1, w // 2 - step + 1, w // 2 + step  # zone rows r0.., columns c0..c1-1
+    k0, k1 = c0 // 2, (c1 - 1) // 2 + 1  # words holding zone pixels
+    top, bottom = (A, B) if first == "A" else (B, A)
+    words[r0:r0 + 54, k0:k1] = top
+    words[r0 + 54:r0 + 108, k0:k1] = bottom
+    return words.reshape(-1)
+
+
+def test_batch_auto_range_pass2_ties(hsv, oracle_mod, table):
+    """The chunked kernel's second pass (operator.hip: the last occurrences of
+    values tied at the maximum count) decides frames where several values
+    share a channel's maximum count: the sequential arg-max (strict >) picks
+    the value whose last occurrence comes first, which need not be the
+    smallest tied value that pass 1 alone would give.  520 VGA frames: every
+    4th a constructed tie in all three channels (_tie_frame, A or B first),
+    the rest uniform bytes.  The test asserts that the tie frames are ones
+    where pass 2 changes the answer, and that every frame equals the oracle."""
+    import torch
+
+    w, h, ll, n = 640, 480, 1280, 520
+    fb = h * ll
+    dev = torch.empty(n * fb, dtype=torch.uint8, device="cuda")
+    hsv.synth(dev, w, h, ll, LAYOUT_YUYV, 0, SEED + 11, first_frame=0)
+    ties = {f: ("A" if f % 8 == 0 else "B") for f in range(0, n, 4)}
+    for f, first in ties.items():
+        dev[f * fb:(f + 1) * fb] = torch.from_numpy(_tie_frame(w, h, ll, first)).cuda()
+    got = hsv.batch_auto_range(dev, w, h, ll, LAYOUT_YUYV).cpu().numpy().astype(np.int64)
+    host = dev.cpu().numpy()
+    decisive = set()
+    for f in ties:
+        for ch in _zone_hsv(table, host[f * fb:(f + 1) * fb], w, h, ll):
+            cnt = np.bincount(ch, minlength=256)
+            tied = np.flatnonzero(cnt == cnt.max())
+            assert tied.size == 2, f
+            last = {int(v): int(np.flatnonzero(ch == v)[-1]) for v in tied}
+            if min(last, key=last.get) != int(tied[0]):
+                decisive.add(f)
+    assert decisive == set(ties), "every tie frame has a channel where pass 2 changes the answer"
+    assert got.tolist() == _auto_want(oracle_mod, host, fb, n, w, h, ll, LAYOUT_YUYV)
 
 
 @pytest.mark.parametrize("w,h,ll,ow,oh,oll,layout,kind", [

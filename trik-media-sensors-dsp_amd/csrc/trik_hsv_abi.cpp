@@ -344,6 +344,7 @@ struct TrikCvHandle {
   // share not being known yet; pending_set holds the costs), resolved by
   // trik_hsv_last_hot_kernel
   std::atomic<int> hot{TRIK_HSV_HOT_AUTO};
+  std::atomic<int> reserved_cus{0};  // trik_hsv_set_reserved_cus
   std::vector<int8_t> hot_groups;
   TableSet* pending_set = nullptr;
 
@@ -378,6 +379,9 @@ struct TrikCvHandle {
   unsigned long long* d_frame_acc = nullptr;  // [frames][16]: 12 sums, the unit count
   int64_t frame_acc_cap = 0;  // frames
   StreamUses fused_users;
+  // the chroma-run kernel's sink for its past-the-end loads (KernelArgs::tail):
+  // kChromaTailSink bytes, allocated once on first use, never resized
+  uint8_t* d_tail_sink = nullptr;
 
   // ov7670 multi-blob sensor: BitmapBuilder's sticky range (uninitialised in
   // the reference before the first setHsvRange; zero here) and scratch
@@ -386,6 +390,7 @@ struct TrikCvHandle {
   size_t d_meta_cap = 0;
   int32_t* d_blob_stats = nullptr;
   size_t d_blob_stats_cap = 0;
+  bool blob_stats_dirty = false;  // zeroed whole by the next call (a failed clusterer launch)
   int32_t* d_blob_top = nullptr;
   size_t d_blob_top_cap = 0;
   TrikHsvTarget* d_blob_targets = nullptr;
@@ -413,6 +418,7 @@ void free_resources(TrikCvHandle* h) {
   h->marks.release();
   (void)hipFree(h->d_wg_part);
   (void)hipFree(h->d_frame_acc);
+  (void)hipFree(h->d_tail_sink);
   (void)hipFree(h->d_frame);
   (void)hipFree(h->d_maps);
   (void)hipFree(h->d_preview);
@@ -439,6 +445,7 @@ void free_resources(TrikCvHandle* h) {
   h->d_blob_targets = nullptr; h->d_blob_targets_cap = 0;
   h->d_wg_part = nullptr; h->d_wg_cnt = nullptr;
   h->d_frame_acc = nullptr; h->frame_acc_cap = 0;
+  h->d_tail_sink = nullptr;
   h->sums_set = h->pending_set = nullptr;
   h->alg_ready = false;
 }
@@ -817,11 +824,27 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
     rc = ensure_fused_scratch(h, b->n_frames, s);
     if (rc) return rc;
   }
+  bool any_chroma = false;
+  for (HotPlan p : plans) any_chroma = any_chroma || p != kPlanStripe;
+  if (any_chroma && !h->d_tail_sink) {  // (its contents are never used: zeroed once for tidiness)
+    void* p = nullptr;
+    HIP_TRY(hipMalloc(&p, (size_t)kChromaTailSink));
+    HIP_TRY(hipMemsetAsync(p, 0, (size_t)kChromaTailSink, s));
+    h->d_tail_sink = static_cast<uint8_t*>(p);
+  }
+  for (KernelArgs& a : args) {
+    a.tail = h->d_tail_sink;
+    a.tail_bytes = h->d_tail_sink ? kChromaTailSink : 0;
+    a.reserved_cus = h->reserved_cus.load();
+  }
   if (step && !fused && b->n_frames > 0 && sums)  // (frames of zero width or height: zero sums)
     HIP_TRY(hipMemsetAsync(sums, 0, sizeof(TrikHsvTargetSums) * (size_t)b->n_frames * n, s));
   bool gated = false, chroma_ran = false;
   // (an empty batch launches nothing and keeps the last call's answer)
-  if (!args.empty()) h->hot_groups.assign(groups, 0);
+  if (!args.empty()) {
+    h->hot_groups.assign(groups, 0);
+    h->pending_set = nullptr;  // (set again as soon as a group is gated)
+  }
   for (size_t g = 0; g < args.size(); ++g) {
     KernelArgs& a = args[g];
     const HotPlan plan = plans[g];
@@ -864,6 +887,7 @@ int32_t run_sums(TrikCvHandle* h, const TrikHsvFrameBatch* b,
         }
         HIP_TRY(e);  // never an ungated launch after a gated one
         h->hot_groups[g] = (int8_t)-partner;
+        h->pending_set = t;  // at once: a later group's error return leaves it consistent
         t->probes[g].mixed = true;
         gated = true;
         continue;
@@ -1119,10 +1143,22 @@ int32_t ensure_blob_scratch(TrikCvHandle* h, int n, int w, int hgt, hipStream_t 
   HIP_TRY(h->blob_users.order_after(s));
   int32_t r = grow(h->d_meta, h->d_meta_cap, nn * (bw * bh > 0 ? bw * bh : 1));
   // the clusterer's own statistics: zero when allocated, and every clusterer
-  // launch leaves the labels it used zero again (blob_ccl_kernel)
-  const bool fresh_stats = nn * 3 * ml * sizeof(int32_t) > h->d_blob_stats_cap;
-  if (!r) r = grow(h->d_blob_stats, h->d_blob_stats_cap, nn * 3 * ml * sizeof(int32_t));
-  if (!r && fresh_stats) HIP_TRY(hipMemsetAsync(h->d_blob_stats, 0, h->d_blob_stats_cap, s));
+  // launch leaves the labels it used zero again (blob_ccl_kernel).  The
+  // capacity counts only once the zeroing is enqueued, and a failed clusterer
+  // launch (which may leave labels non-zero) marks the buffer dirty: the next
+  // call zeroes it whole.
+  const size_t stats_bytes = nn * 3 * ml * sizeof(int32_t);
+  if (!r && (stats_bytes > h->d_blob_stats_cap || h->blob_stats_dirty)) {
+    if (stats_bytes > h->d_blob_stats_cap) r = grow(h->d_blob_stats, h->d_blob_stats_cap, stats_bytes);
+    if (!r) {
+      const hipError_t e = hipMemsetAsync(h->d_blob_stats, 0, h->d_blob_stats_cap, s);
+      if (e != hipSuccess) {
+        h->blob_stats_dirty = true;
+        return fail(TRIK_IVIDTRANSCODE_EFAIL, std::string("hipMemsetAsync(blob stats): ") + hipGetErrorString(e));
+      }
+      h->blob_stats_dirty = false;
+    }
+  }
   if (!r) r = grow(h->d_blob_top, h->d_blob_top_cap, nn * 24 * sizeof(int32_t));
   if (!r) r = grow(h->d_blob_targets, h->d_blob_targets_cap, nn * 8 * sizeof(TrikHsvTarget));
   return r;
@@ -1178,7 +1214,11 @@ int32_t run_blob(TrikCvHandle* h, BlobArgs& ba, TableSet& t, hipStream_t s) {
     h->pending_set = &t;
     h->hot_groups[0] = -TRIK_HSV_HOT_STRIPE;
   }
-  HIP_TRY(launch_blob(ba, s));
+  const int e = launch_blob(ba, s);
+  if (e != hipSuccess) {
+    h->blob_stats_dirty = true;  // (the clusterer may not have restored its statistics to zero)
+    return fail(TRIK_IVIDTRANSCODE_EFAIL, std::string("launch_blob: ") + hipGetErrorString((hipError_t)e));
+  }
   return 0;
 }
 
@@ -1722,6 +1762,11 @@ std::string device_buffer_error(const void* p, int dev, const char* what) {
 extern "C" int32_t trik_hsv_set_hot_kernel(TRIK_VIDTRANSCODE_CV_Handle h, int32_t kind) {
   if (!h || kind < TRIK_HSV_HOT_AUTO || kind > TRIK_HSV_HOT_GENERIC) return -1;
   return h->hot.exchange(kind);
+}
+
+extern "C" int32_t trik_hsv_set_reserved_cus(TRIK_VIDTRANSCODE_CV_Handle h, int32_t n) {
+  if (!h || n < 0 || n > 32) return -1;
+  return h->reserved_cus.exchange(n);
 }
 
 extern "C" int32_t trik_hsv_last_hot_kernel(TRIK_VIDTRANSCODE_CV_Handle h) {

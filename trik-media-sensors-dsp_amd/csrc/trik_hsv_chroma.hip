@@ -84,8 +84,8 @@ constexpr uint32_t kLdsRuns = kLdsVal + 256;          // u16 [65536] b1 | b2 << 
 constexpr uint32_t kLdsQueues = kLdsRuns + 131072;    // blob kernel: per wave kQueueCap x {word, pos}
 static_assert(kLdsBlocks + 8192 <= kLdsPairs, "LDS layout");
 // hot kernel records: per wave kRecCap x 16 B of words, then all waves' meta
-// words (kRecCap x 4 B per wave): f (bits 0-3: the piece's flagged words) |
-// x / 8 (bits 4-15) | row in the tile (bits 16-31)
+// words (kRecCap x 4 B per wave): f (bits 0-3: the piece's flagged words,
+// bit 3 - j = word j) | x / 8 (bits 4-15) | row in the tile (bits 16-31)
 constexpr uint32_t kLdsRecWords = kLdsQueues;
 constexpr uint32_t kLdsRecMeta = kLdsRecWords + kHotWaves * kRecCap * 16;
 // fused step: the workgroup's 12 u64 totals (3 per range)
@@ -209,12 +209,15 @@ __device__ __forceinline__ uint4 ld_nt16(const uint8_t* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-// v if this lane's bit of wave mask m is set, else 0 (one v_cndmask; a
-// v_addc shift-in chain needs a wait state after every op on gfx950)
-__device__ __forceinline__ uint32_t lane_bit(uint64_t m, uint32_t v) {
-  return __builtin_amdgcn_inverse_ballot_w64(m) ? v : 0u;
+// 2 v + (this lane's bit of wave mask m): one v_addc_co_u32 with the mask as
+// its carry-in (a record's flag bits, shifted in word by word; the carry-in
+// is written by SALU, no wait state)
+__device__ __forceinline__ uint32_t shift_in(uint32_t v, uint64_t m) {
+  uint32_t r;
+  uint64_t co;
+  asm volatile("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=&s"(co) : "v"(v), "s"(m));
+  return r;
 }
-
 // 4-bit mask (range t -> bit t) -> byte-spread (range t -> bit 8t)
 __device__ __forceinline__ uint32_t spread4(uint32_t m) { return (m * 0x00204081u) & 0x01010101u; }
 
@@ -627,7 +630,8 @@ struct ChromaGeom {
   // ceil(2^20 / cpr), exact for lt < 1024 and cpr < 1024
   FastDiv fd_units, fd_tiles;
   uint32_t cpr_inv;
-  int32_t tail_ok;  // the past-the-end loads fit inside the ChromaTables block
+  int32_t tail_ok;  // the past-the-end loads read the handle's sink (KernelArgs::tail)
+  int64_t tail_span;  // bytes from a tile's base those loads span (chroma_tail_span)
   int32_t units;  // wave-sized units per tile: ceil(k * cpr / 64) <= kHotWaves
 };
 
@@ -862,7 +866,7 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
       const uint32_t meta = act ? *(lds32_t)(uintptr_t)(rm_s + 4u * (base + (uint32_t)lane)) : 0u;
       const uint32_t fl = meta & 15u;
       if (act) {
-        const uint32_t i = (uint32_t)__builtin_ctz(fl);
+        const uint32_t i = 3u - (uint32_t)__builtin_ctz(fl);
         const uint32_t w = *(lds32_t)(uintptr_t)(rec + 4u * i);  // the record's first flagged word
         const uint32_t x = ((meta >> 4) & 0xFFFu) * 8u + 2u * i, yr = meta >> 16;
         const uint32_t d = ld16(kLdsRuns + 2u * chroma_of(w));
@@ -958,12 +962,14 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
 #pragma unroll
         for (int i = 0; i < CW; ++i) asm volatile("" : "+v"(d[i]), "+v"(cut[i]));
         // per piece: the lanes with a flagged word (SALU) and the record's
-        // meta word with the flag bits (bit j = word j of the piece), formed
-        // word by word so that each word's flag mask dies at once (held for
-        // the appends, the eight masks pushed the unit's SGPRs into spills)
+        // meta word with the flag bits (bit 3 - j = word j of the piece),
+        // shifted in word by word (one v_addc each, round 6: C3 -0.3 %, C4
+        // -0.8 %, scripts/ab/r06c_flags.py) so that each word's flag mask dies
+        // at once (held for the appends, the eight masks pushed the unit's
+        // SGPRs into spills)
         uint64_t ma = 0, mb = 0;
         const uint32_t meta_a = meta_x | ((uint32_t)(ro + s * g.rstep) << 16);
-        uint32_t fa = meta_a, fb = meta_a + meta_b;
+        uint32_t fa = meta_a >> 4, fb = (meta_a + meta_b) >> 4;  // (flag bits 0-3 of the meta words are 0)
 #pragma unroll
         for (int i = 0; i < CW; ++i) {
           uint64_t q0 = 0, q1 = 0, bal;
@@ -978,12 +984,10 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
           asm volatile("" : "+s"(bal));
           if (i < 4) {
             ma |= bal;
-            fa |= lane_bit(bal, 1u << i);
-            if (i & 1) asm volatile("" : "+v"(fa));  // (two words per v_or3)
+            fa = shift_in(fa, bal);
           } else {
             mb |= bal;
-            fb |= lane_bit(bal, 1u << (i - 4));
-            if (i & 1) asm volatile("" : "+v"(fb));
+            fb = shift_in(fb, bal);
           }
           if (MASKS && (i < 4 ? valid : validb)) {  // verification mode: the exact path writes the flagged pixels
             const int y = y0 + s * g.rstep + (i < 4 ? 0 : half);
@@ -1037,12 +1041,13 @@ __global__ __launch_bounds__(kMaxBlock) void chroma_kernel(KernelArgs a, ChromaG
       // two steps ahead, measured no faster: the kernel is VALU-bound)
       // (the load past the tile's last step is unconditional: that keeps the
       // step's wait at "this step's data", where a branch around it makes the
-      // compiler wait for every load in flight.  It reads the start of the
-      // ChromaTables block, L2-resident, when the lanes' offsets fit inside
-      // it (tail_ok) -- re-reading the tile's last rows instead cost 2.2 %
-      // extra HBM reads, scripts/ab/r05s_tail.py)
+      // compiler wait for every load in flight.  Its data is never used.  It
+      // reads the handle's L2-resident sink when the lanes' offsets fit inside
+      // it (tail_ok: chroma_tail_span <= KernelArgs::tail_bytes, checked on
+      // the host) -- re-reading the tile's last rows instead cost 2.2 % extra
+      // HBM reads, scripts/ab/r05s_tail.py -- and otherwise those rows)
       const uint8_t* rb = tbase;
-      const uint8_t* const tail = reinterpret_cast<const uint8_t*>(ct);
+      const uint8_t* const tail = a.tail;
       auto ld = [&](int s, uint32_t (&w)[CW]) {
         if (FULL) load_chunk<LAYOUT>(rb + voff, rb + hb + voff, plane, w);
         else
@@ -1336,7 +1341,10 @@ int launch_t(const KernelArgs& a, const ChromaGeom& g, const ChromaTables* ct, h
   auto kern = chroma_kernel<LAYOUT, NR, MASKS>;
   hipError_t e = set_dynamic_lds(reinterpret_cast<const void*>(kern), (int)kLdsBytes);
   if (e != hipSuccess) return e;
-  const int cus = device_cus();
+  // one workgroup per CU the stream may use (a CU-masked stream: its mask),
+  // less the CUs left free for kernels on other streams
+  const int cus_all = stream_cus(s);
+  const int cus = cus_all - a.reserved_cus >= 1 ? cus_all - a.reserved_cus : 1;
   const int block = 64 * kHotWaves;
   const int64_t grid = g.n_tiles < cus ? g.n_tiles : cus;  // one workgroup per CU (LDS image)
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(block), kLdsBytes, s, a, g, ct);
@@ -1411,10 +1419,12 @@ bool chroma_geometry(const KernelArgs& a, ChromaGeom& g) {
   int r = 65535 / (2 * span);
   g.flush_rounds = r > 127 ? 127 : r;
   g.units = (g.k * g.cpr + 63) / 64;
-  // the past-the-end loads may read the ChromaTables block instead (YUYV: a
-  // lane's two loads lie within (k + dy) rows + 2 dx bytes of the base; the
-  // ov7670 layout's second load is a whole luma plane further: never)
-  g.tail_ok = split && (int64_t)(g.k + g.dy) * a.line_length + 2LL * g.dx + 16 <= (int64_t)sizeof(ChromaTables);
+  // the past-the-end loads read the handle's sink when the lanes' offsets fit
+  // (YUYV: a lane's two loads lie within (k + dy) rows + 2 dx bytes of the
+  // tile base; ov7670: within k rows of it and of the chroma plane H rows on)
+  g.tail_span = split ? (int64_t)(g.k + g.dy) * a.line_length + 2LL * g.dx + 16
+                      : (int64_t)a.height * a.line_length + (int64_t)g.k * a.line_length + 16;
+  g.tail_ok = a.tail != nullptr && g.tail_span <= a.tail_bytes;
   g.fd_units = make_div((uint32_t)g.units);
   g.fd_tiles = make_div((uint32_t)g.tiles_per_frame);
   g.cpr_inv = (uint32_t)(((1u << 20) + (uint32_t)cpr - 1) / (uint32_t)cpr);
@@ -1424,6 +1434,11 @@ bool chroma_geometry(const KernelArgs& a, ChromaGeom& g) {
 bool chroma_geometry_ok(const KernelArgs& a) {
   ChromaGeom g;
   return chroma_geometry(a, g);
+}
+
+int64_t chroma_tail_span(const KernelArgs& a) {
+  ChromaGeom g;
+  return chroma_geometry(a, g) ? g.tail_span : -1;
 }
 
 // The fused step splits the units evenly over the workgroups and completes
@@ -1440,6 +1455,8 @@ int launch_chroma(const KernelArgs& a, const ChromaTables* ct, bool write_masks,
   if (g.n_tiles == 0) return hipSuccess;
   if (a.fused && (write_masks || !chroma_fused_ok(a) || !a.wg_part || !a.wg_cnt || !a.frame_acc))
     return hipErrorInvalidValue;
+  // every lane's past-the-end load stays inside the sink (or is not redirected)
+  if (g.tail_ok && (g.tail_span > a.tail_bytes || g.tail_span <= 0)) return hipErrorInvalidValue;
   if (a.layout == TRIK_HSV_LAYOUT_YUYV)
     return write_masks ? launch_nr<TRIK_HSV_LAYOUT_YUYV, true>(a, g, ct, s)
                        : launch_nr<TRIK_HSV_LAYOUT_YUYV, false>(a, g, ct, s);

@@ -29,6 +29,19 @@ int device_cus() {
   return n;
 }
 
+int stream_cus(hipStream_t s) {
+  const int all = device_cus();
+  if (!s) return all;
+  // a stream created with a CU mask (hipExtStreamCreateWithCUMask) runs its
+  // kernels on the masked CUs only: one workgroup per CU means one per
+  // masked CU (the rest would wait for a second round)
+  uint32_t m[32] = {};
+  if (hipExtStreamGetCUMask(s, 32, m) != hipSuccess) return all;
+  int n = 0;
+  for (uint32_t w : m) n += __builtin_popcount(w);
+  return n > 0 && n < all ? n : all;
+}
+
 hipError_t set_dynamic_lds(const void* kern, int bytes) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);

@@ -155,6 +155,14 @@ struct KernelArgs {
   unsigned long long* wg_part = nullptr;  // scratch: [workgroups][12]
   uint32_t* wg_cnt = nullptr;             // scratch: 0 between launches
   unsigned long long* frame_acc = nullptr;  // scratch: [n_frames][16], 0 between launches
+  // The chroma-run kernel's past-the-end loads (one per lane and tile, never
+  // consumed) read this per-handle sink instead of the frames when the
+  // lane's offsets fit (chroma_tail_span() <= tail_bytes); otherwise they
+  // re-read the tile's last rows.  No load depends on another allocation.
+  const uint8_t* tail = nullptr;
+  int64_t tail_bytes = 0;
+  // CUs the chroma-run kernel leaves free (trik_hsv_set_reserved_cus)
+  int32_t reserved_cus = 0;
 };
 
 // The target of one (frame, range) from its sums: WSEQ:486-505 (unsigned
@@ -257,6 +265,9 @@ struct LineArgs {
 // the current device's CU count, and a kernel's dynamic-LDS attribute set once
 // per (device, kernel).
 int device_cus();
+// the CUs stream s may use: its CU mask's (hipExtStreamCreateWithCUMask), else
+// the device's
+int stream_cus(hipStream_t s);
 hipError_t set_dynamic_lds(const void* kern, int bytes);
 
 // Launchers (trik_hsv_kernels.hip, trik_hsv_operator.hip, trik_hsv_line.hip).
@@ -274,6 +285,13 @@ bool chroma_geometry_ok(const KernelArgs& a);
 // verification masks)
 bool chroma_fused_ok(const KernelArgs& a);
 int launch_chroma(const KernelArgs& a, const ChromaTables* ct, bool write_masks, hipStream_t s);
+// Bytes from a tile's base that the chroma-run kernel's past-the-end loads
+// span for this geometry (YUYV: (k + dy) rows + 2 dx; ov7670: a luma plane
+// and k rows), or -1 when the kernel does not take the geometry.
+int64_t chroma_tail_span(const KernelArgs& a);
+// The per-handle sink's size: spans up to this read the sink (ov7670 frames
+// up to ~2 Mpixel), larger ones re-read the tile's last rows.
+constexpr int64_t kChromaTailSink = 4 << 20;
 // Sets the calling thread's trik_hsv_last_error() message; returns code.
 int32_t set_error(int32_t code, const std::string& msg);
 // The packed ranges of up to kTableGroups groups of <= 4 (kernel argument).

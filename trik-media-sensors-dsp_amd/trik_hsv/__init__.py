@@ -92,6 +92,14 @@ class _HotKernel:
         """The kernel this handle's last hot launch ran."""
         return _lib.trik_hsv_last_hot_kernel(self._h)
 
+    def set_reserved_cus(self, n: int) -> int:
+        """CUs the chroma-run kernel leaves free for kernels on other streams
+        (trik_hsv_set_reserved_cus).  Returns the previous setting."""
+        prev = _lib.trik_hsv_set_reserved_cus(self._h, int(n))
+        if prev < 0:
+            raise ValueError(f"reserved CUs out of range: {n}")
+        return prev
+
 
 class Detector(_HotKernel):
     """Batched HSV-threshold + centroid over frames resident in device memory.

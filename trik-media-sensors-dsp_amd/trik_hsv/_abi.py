@@ -202,6 +202,7 @@ PROTOTYPES = {
     "trik_hsv_synth": ([C.POINTER(FrameBatch), i32, i32, u64, C.c_void_p], i32),
     "trik_hsv_set_hot_kernel": ([C.c_void_p, i32], i32),
     "trik_hsv_last_hot_kernel": ([C.c_void_p], i32),
+    "trik_hsv_set_reserved_cus": ([C.c_void_p, i32], i32),
     "trik_hsv_chroma_share": ([C.c_void_p, C.POINTER(C.c_double)], i32),
     "trik_hsv_chroma_measured_share": ([C.c_void_p, C.POINTER(C.c_double)], i32),
     # XDAIS IALG functions (also in the exported function tables)
