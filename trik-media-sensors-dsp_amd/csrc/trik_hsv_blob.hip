@@ -254,7 +254,7 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
   // per row); pf: the next batch.  Loads take clamped columns and rows (no
   // branches); columns past the row are masked when a batch is taken.
   constexpr int RB = KMAX <= 5 ? 8 : 1;
-  uint32_t pf[RB][KMAX], bt[RB][KMAX];
+  uint32_t pf[RB][KMAX], bt[KMAX];  // bt: the current batch as bits (bit i = its row i), shifted a row per row
   // (LDS-staged or global: separate paths, so that neither is a flat load --
   // a flat load in flight would hold every LDS wait of the row too)
   // (the staged copy at its LDS offset: the dynamic LDS starts at 0)
@@ -276,28 +276,35 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
   };
   if (bh > 0) load_batch(0);
   int next = 1;  // next new label (wave-uniform)
+  // the lane's statistics run: label acc_l's (x, y, size) so far, added to
+  // the label's sums when the lane meets another label (in its columns, row
+  // after row) and at the end -- a blob's columns keep their label for many
+  // rows, so a lane adds once per blob, not once per row (the adds in flight
+  // sit in every row batch's memory wait)
+  uint32_t acc_l = 0;
+  int32_t ax = 0, ay = 0, an = 0;
   for (int r = 0; r < bh; ++r) {
     if (r % RB == 0) {  // take the batch in flight, start the next one
 #pragma unroll
-      for (int i = 0; i < RB; ++i)
+      for (int j = 0; j < KMAX; ++j) {
+        uint32_t v = 0;
 #pragma unroll
-        for (int j = 0; j < KMAX; ++j) bt[i][j] = (j < K && c0 + j < bw) ? pf[i][j] : 0u;
+        for (int i = 0; i < RB; ++i) v |= (pf[i][j] & 1u) << i;
+        bt[j] = (j < K && c0 + j < bw) ? v : 0u;
+      }
       load_batch(r + RB);  // (unconditional: past the last row it re-reads it; a branch here
                            // made the compiler copy, and so wait for, the new loads)
     }
     uint32_t prev_last = 0, d_last = 0;
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) {
-      dd[j] = bt[0][j];
+      dd[j] = bt[j] & 1u;
+      bt[j] >>= 1;
       if (j == K - 1) {
         prev_last = prv[j];
         d_last = dd[j];
       }
     }
-#pragma unroll
-    for (int i = 0; i + 1 < RB; ++i)
-#pragma unroll
-      for (int j = 0; j < KMAX; ++j) bt[i][j] = bt[i + 1][j];
     // a row without a set metapixel opens, joins and counts nothing (CLU:98-112
     // only acts on set ones): its labels are 0 -- skip the scans (camera-like
     // frames are mostly such rows)
@@ -389,8 +396,6 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
     // labels; equivalence events flagged
     uint32_t events = 0;  // bit j: column c0 + j has a neighbour label != L
     {
-      uint32_t acc_l = 0;
-      int32_t ax = 0, ay = 0, an = 0;
 #pragma unroll
       for (int j = 0; j < KMAX; ++j) {
         const uint32_t L = cur[j];
@@ -411,7 +416,6 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
         }
         if (labels && j < K && c0 + j < bw) labels[(int64_t)r * bw + c0 + j] = (uint16_t)L;
       }
-      if (an) add_own(acc_l, ax, ay, an);
     }
     // equivalence events in raster order: lane by lane, each lane in column
     // order (CLU:92-96 as eq[a] = eq[L] for every non-zero neighbour a)
@@ -439,6 +443,7 @@ __global__ __launch_bounds__(64) void blob_ccl_kernel(BlobArgs a) {
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) prv[j] = cur[j];
   }
+  if (an) add_own(acc_l, ax, ay, an);
   __threadfence();
   __syncthreads();
   const int n = next;
