@@ -8,6 +8,10 @@
 //             s_and_b64 straight into VCC): +2 SALU per word
 //   word_pipe word_e64's two words interleaved: both words' compares, then
 //             their SALU combines, then their selects
+//   form_cmp  the shipped word form (compares into SGPR masks, selects) with the
+//             pair counter, the odd-pixel counter and the flag mask; the
+//             "per VALU instruction" column is per WORD here
+//   form_swar the same outputs by a SWAR form (swar_word: VERDICT r5 lever a)
 //   cnd_e64   4 v_cndmask_b32_e64 + v_add3 alone (masks in SGPRs)
 //   cnd_e32   the same as v_cndmask_b32_e32, VCC from s_mov_b64 before each
 // Two independent words per iteration.
@@ -240,6 +244,76 @@ __global__ __launch_bounds__(256) void word_pipe(uint32_t* out, uint32_t seed) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = P ^ P2 ^ d;
 }
 
+
+// The VERDICT r5 lever (a): a SWAR fast path for one YUYV word -- both
+// pixels' Y against broadcast thresholds in 16-bit lanes with a guard bit
+// (Y + 256 - t: bit 8 of a lane set iff Y >= t), the classes by bit logic,
+// the byte-spread masks weighted by the classes' pixel counts
+// (v_mad_u32_u24), the word's flag by one compare.  Same outputs as the
+// shipped select (the pair counter P, the odd-pixel counter O, the flag mask).
+__device__ __forceinline__ void swar_word(uint32_t w, uint32_t d, uint32_t bw, uint32_t m1, uint32_t m2,
+                                          uint32_t& P, uint32_t& O, uint64_t& q) {
+  const uint32_t Z = (w & 0x00FF00FFu) | 0x01000100u;             // [Y0 + 256, Y1 + 256]
+  const uint32_t T1 = __builtin_amdgcn_perm(0u, d, 0x0C000C00u);   // [b1, b1]
+  const uint32_t T2 = __builtin_amdgcn_perm(0u, d, 0x0C010C01u);   // [b2, b2]
+  const uint32_t TA = __builtin_amdgcn_perm(0u, bw, 0x0C010C01u);  // [A, A]
+  const uint32_t ge1 = Z - T1, gt2 = Z - 0x00010001u - T2, geA = Z - TA;
+  const uint32_t c1 = geA & ~(ge1 | gt2) & 0x01000100u;  // A <= Y < b1, Y <= b2: M1
+  const uint32_t c2 = geA & ge1 & ~gt2 & 0x01000100u;    // A <= Y, b1 <= Y <= b2: M2
+  const uint32_t fl = ~ge1 & gt2 & 0x01000100u;          // b2 < Y < b1: the exact path
+  const bool x = d == 0x00FFu;
+  uint32_t es = __umul24((uint32_t)__builtin_popcount(c1), m1) + __umul24((uint32_t)__builtin_popcount(c2), m2);
+  uint32_t e1 = __umul24(c1 >> 24, m1) + __umul24(c2 >> 24, m2);
+  P += x ? 0u : es;
+  O += x ? 0u : e1;
+  q |= __builtin_amdgcn_ballot_w64(fl != 0u || x);
+}
+
+// the shipped select in C form (select2w's compares and selects) with the
+// same outputs, for a like-for-like count
+__device__ __forceinline__ void cmp_word(uint32_t w, uint32_t d, uint32_t bw, uint32_t m1, uint32_t m2,
+                                         uint32_t& P, uint32_t& O, uint64_t& q) {
+  uint64_t x, lt0, lt1, le0, le1, ge0, ge1;
+  asm volatile(CMPS("%[x]", "%[lt0]", "%[lt1]", "%[le0]", "%[le1]", "%[ge0]", "%[ge1]", "%[d]", "%[a]", "%[w]")
+               "s_nop 0"
+               : [x] "=&s"(x), [lt0] "=&s"(lt0), [lt1] "=&s"(lt1), [le0] "=&s"(le0), [le1] "=&s"(le1),
+                 [ge0] "=&s"(ge0), [ge1] "=&s"(ge1)
+               : [w] "v"(w), [d] "v"(d), [a] "v"(bw), [k] "s"(0xFFu));
+  q |= x | (lt0 & ~le0) | (lt1 & ~le1);
+  const uint64_t k0 = le0 & ge0 & ~x, k1 = le1 & ge1 & ~x;
+  uint32_t e0, e1;
+  asm volatile(
+      "v_cndmask_b32_e64 %[e0], %[m2], %[m1], %[lt0]\n\t"
+      "v_cndmask_b32_e64 %[e1], %[m2], %[m1], %[lt1]\n\t"
+      "v_cndmask_b32_e64 %[e0], 0, %[e0], %[k0]\n\t"
+      "v_cndmask_b32_e64 %[e1], 0, %[e1], %[k1]"
+      : [e0] "=&v"(e0), [e1] "=&v"(e1)
+      : [m1] "v"(m1), [m2] "v"(m2), [lt0] "s"(lt0), [lt1] "s"(lt1), [k0] "s"(k0), [k1] "s"(k1));
+  P = P + e0 + e1;
+  O += e1;
+}
+
+template <bool SWAR>
+__global__ __launch_bounds__(256) void word_form(uint32_t* out, uint32_t seed) {
+  uint32_t w = seed * 0x9E3779B9u + threadIdx.x * 0x85EBCA6Bu, w2 = w ^ 0x1234567u;
+  uint32_t d = (w ^ 0x5bd1e995u) & 0xFFFFu, bw = (w * 3u) & 0xFFFFu, m1 = (w * 7) & 0x01010101u, m2 = (w * 13) & 0x01010101u;
+  uint32_t P = 0, P2 = 0, O = 0;
+  uint64_t q = 0;
+  for (int i = 0; i < ITERS; ++i) {
+    if (SWAR) {
+      swar_word(w, d, bw, m1, m2, P, O, q);
+      swar_word(w2, d, bw, m1, m2, P2, O, q);
+    } else {
+      cmp_word(w, d, bw, m1, m2, P, O, q);
+      cmp_word(w2, d, bw, m1, m2, P2, O, q);
+    }
+    w += 0x01000101u;
+    w2 += 0x00010001u;
+    d ^= (uint32_t)q & 0xFFu;
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = P ^ P2 ^ O ^ (uint32_t)q;
+}
+
 template <typename K>
 void run(const char* name, K kern, double instr_per_iter, int cus, int clk, uint32_t* out) {
   hipEvent_t a, b;
@@ -271,6 +345,8 @@ int main() {
   run("word_e64", word_e64, 24, cus, clk, out);  // 2 words x (7 cmp + 4 cndmask + 1 add3)
   run("word_e32", word_e32, 24, cus, clk, out);
   run("word_pipe", word_pipe, 24, cus, clk, out);
+  run("form_cmp", word_form<false>, 2, cus, clk, out);  // per word (2 words per iteration)
+  run("form_swar", word_form<true>, 2, cus, clk, out);
   run("cnd_e64", cnd_e64, 10, cus, clk, out);
   run("cnd_e32", cnd_e32, 10, cus, clk, out);
   return 0;

@@ -644,6 +644,10 @@ __global__ __launch_bounds__(kRangeBlock) void auto_range_vec_kernel(AutoRangeAr
       load_batch(j0, w, row, x0, ok);
 #pragma unroll
       for (int b = 0; b < kVecBatch; ++b) {
+        // a batch slot past the zone for the whole wave: no HSV to compute
+        // (the last batch of a VGA frame's 3,180 chunks fills 108 of its
+        // 1,024 slots)
+        if (__builtin_amdgcn_ballot_w64(ok[b]) == 0ull) continue;
 #pragma unroll
         for (int i = 0; i < NW; ++i) {
           const int c = x0[b] + 2 * i;
