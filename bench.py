@@ -303,8 +303,9 @@ def main():
                                  "k+1's kernel runs; step k+2 waits for it on the device",
                       "reserved_cus": args.reserve_cus,
                       "overlap_evidence": "the hot kernel holds one 160-KiB-LDS workgroup on every CU it is given; "
-                                          "a kernel on another stream runs beside it only on CUs left free "
-                                          "(profiles/r06/overlap_*: scripts/overlap_probe.py traces)",
+                                          "a kernel on another stream runs beside it on CUs left free (reserved_cus) "
+                                          "or takes a CU before the hot workgroup for it starts; rocprofv3 traces: "
+                                          "profiles/r06/r06d_overlap_*_trace.txt (scripts/overlap_probe.py)",
                       "tests": "one-rank comm (tests/test_gpu_multirank.py::test_bench_library_comm_one_rank); "
                                "two ranks over nccl: test_bench_two_ranks_library_comm_nccl (runs where 2 GPUs "
                                "are visible)"}
