@@ -1,7 +1,7 @@
 """Auto-range batch timing on two inputs (development timing of the in-tree
 library variant): the synthetic scene of bench_operator.py and uniform random
 bytes (every lane of a wave on its own H/S/V bin -- the worst case for the
-wave-peeled histogram atomics).  usage: python scripts/range_time.py [--frames N]"""
+wave-peeled histogram atomics).  usage: python scripts/range_time.py [--frames N] [--only scene|random]"""
 import argparse
 import json
 import os
@@ -13,6 +13,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=4096)
+    ap.add_argument("--only", choices=["scene", "random"], default=None)
     args = ap.parse_args()
     import torch
 
@@ -20,7 +21,7 @@ def main():
     W, H, LL, F = 640, 480, 1280, args.frames
     dev = torch.empty(F * H * LL, dtype=torch.uint8, device="cuda")
     out = {"lib": "in-tree"}
-    for name in ("scene", "random"):
+    for name in ((args.only,) if args.only else ("scene", "random")):
         if name == "scene":
             trik_hsv.synth(dev, W, H, LL, trik_hsv.LAYOUT_YUYV, 1, 0x7A1C)
         else:

@@ -188,6 +188,36 @@ def test_batch_auto_range_fallback_kernels(hsv, oracle_mod, w, h, ll, layout, n,
     assert got.tolist() == _auto_want(oracle_mod, host, fb, n, w, h, ll, layout)
 
 
+def test_batch_auto_range_single_colour_frames(hsv, table):
+    """Every (U, V) at six Y levels, one colour per frame (96x24, a 7x7 zone,
+    393,216 frames): each channel's winner is the colour's own H, S and V, so
+    the output is (H x 1.4, S x 0.39, V x 0.39) with the reference's float
+    constants (hpp:190-195) -- the chunked kernel's packed two-pixel HSV
+    (hsv_key2: both pixels of a word in 16-bit halves, the B channel's 16-bit
+    wrap) against the oracle's table on every one of those (Y, U, V).  H is
+    checked exactly (1.4 H is injective), S and V through the scaling."""
+    import torch
+
+    w, h, ll = 96, 24, 192
+    ys = [0, 37, 100, 160, 222, 255]
+    uv = np.arange(65536, dtype=np.int64)
+    U, V = uv & 255, uv >> 8
+    Y = np.repeat(np.array(ys, np.int64), 65536)
+    U, V = np.tile(U, len(ys)), np.tile(V, len(ys))
+    word = Y | (U << 8) | (Y << 16) | (V << 24)
+    word = np.where(word >= 1 << 31, word - (1 << 32), word).astype(np.int32)
+    n, per = word.size, h * ll // 4
+    dev = torch.from_numpy(word).cuda().view(-1, 1).expand(n, per).contiguous().view(torch.uint8).reshape(-1)
+    got = hsv.batch_auto_range(dev, w, h, ll, LAYOUT_YUYV).cpu().numpy().astype(np.int64)
+    e = table[Y | (U << 8) | (V << 16)] & 0xFFFFFFFF
+    H, S, Vv = e & 0xFF, (e >> 8) & 0xFF, (e >> 16) & 0xFF
+    k14, k39 = np.float64(np.float32(1.4)), np.float64(np.float32(0.39))
+    want = np.stack([(H * k14).astype(np.uint16), np.full(n, 15), (S * k39).astype(np.uint16), np.full(n, 30),
+                     (Vv * k39).astype(np.uint16), np.full(n, 30)], 1).astype(np.int64)
+    bad = np.flatnonzero((got != want).any(1))
+    assert bad.size == 0, [(int(Y[i]), int(U[i]), int(V[i]), got[i].tolist(), want[i].tolist()) for i in bad[:5]]
+
+
 def _zone_hsv(table, fr, w, h, ll):
     """The strict central zone's per-pixel (H, S, V) of a YUYV frame in scan
     order (cv_hsv_range_detector.hpp:88-108 bounds), from the oracle's table."""

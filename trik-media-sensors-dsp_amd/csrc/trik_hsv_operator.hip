@@ -547,9 +547,10 @@ __global__ __launch_bounds__(kBlock) void auto_range_kernel(AutoRangeArgs a) {
 //    chunks tid, tid + 256, ... in batches of kVecBatch with every load of a
 //    batch in flight (the one-pixel-per-lane walk waited one load latency per
 //    pixel).
-//  * Pass 1 counts only: a lane run-length encodes the (H, S, V) triples of
-//    its pixels in scan order and adds each run once per channel to its
-//    wave's LDS histograms (one atomic per run, not per pixel).
+//  * Pass 1 counts only: a lane run-length encodes each of H, S, V of its
+//    pixels in scan order and adds each run once to its wave's LDS
+//    histogram of that channel (one atomic per run, not per pixel); the two
+//    pixels of a word share one packed HSV computation (hsv_key2).
 //  * The winner of a channel whose maximum count M is held by one value is
 //    that value.  Only channels where several values reach M need their last
 //    occurrences (see the file comment): pass 2 recomputes the zone's HSV and
@@ -562,25 +563,72 @@ struct AutoVecGeom {
   uint32_t total;      // zone rows * chunks per row
 };
 
-// (H | S << 8 | V << 16) of pixel P of the YUYV-ordered word w (Y0 U Y1 V):
-// hsv_bytes' arithmetic on a word in registers
-template <int P>
-__device__ __forceinline__ uint32_t hsv_key(uint32_t w, const uint16_t* l43, const uint16_t* l255) {
-  using stripe_px::clamp8_shift6;
-  constexpr uint32_t kY = P == 0 ? 74u : (74u << 16);
-  const uint32_t wc = w ^ 0xFF00FF00u;
-  const int r = clamp8_shift6(__builtin_amdgcn_udot4(w, kY | (102u << 24), (uint32_t)-14248, false));
-  const int g = clamp8_shift6(__builtin_amdgcn_udot4(wc, kY | (25u << 8) | (52u << 24), (uint32_t)-10939, false));
-  const int b = clamp8_shift6(__builtin_amdgcn_udot4(w, kY | (129u << 8), (uint32_t)-17672, false));
-  const int mx = max(r, max(g, b)), mn = min(r, min(g, b));
-  const bool eqG = mx == g, eqB = mx == b;  // priority G > B > R (WSEQ:226-246)
-  const int diff = eqG ? b - r : (eqB ? r - g : g - b);
-  const int base = eqG ? 21845 : (eqB ? 43690 : 0);
-  const uint32_t h = (((uint32_t)(base + (int)l43[mx - mn] * diff)) >> 8) & 0xFFu;
-  const uint32_t s = ((uint32_t)l255[mx] * (uint32_t)(mx - mn)) >> 8;
-  return h | (s << 8) | ((uint32_t)mx << 16);
+// One of R, G, B for both pixels of a word, one per 16-bit half: Y holds Y0
+// and Y1 in its halves, c the channel's chroma term (its low 16 bits, used
+// for both halves).  (74 Y + c) mod 2^16 is the reference's 16-bit _add2 sum
+// (the B channel's wrap included), then >> 6 with the sign of bit 15 and the
+// clamp to [0, 255] (WSEQ:181-205; clamp8_shift6 per pixel).
+__device__ __forceinline__ uint32_t pk_chan(uint32_t Y, uint32_t c) {
+  uint32_t x;
+  asm("v_pk_mad_u16 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(x) : "v"(Y), "v"(74u), "v"(c));
+  asm("v_pk_ashrrev_i16 %0, 6, %0 op_sel_hi:[0,1]" : "+v"(x));
+  asm("v_pk_max_i16 %0, %0, 0" : "+v"(x));
+  asm("v_pk_min_i16 %0, %0, %1 op_sel_hi:[1,0]" : "+v"(x) : "v"(255u));
+  return x;
 }
-
+// (H | S << 8 | V << 16) of both pixels of the YUYV-ordered word w (Y0 U Y1
+// V): WSEQ:207-249 for two pixels at once.  R, G, B, their max, min and the
+// three hue differences in packed 16-bit halves; the hue case selects,
+// LUT43 / LUT255 reads and products per pixel (v_mad_i32_i16 and SDWA take
+// the pixel's half).  52 VALU per word and no branches, against 66 and two
+// divergent branches per pixel for hsv_bytes' form (round 6,
+// scripts/ab/r06q_hsv2.py).
+__device__ __forceinline__ void hsv_key2(uint32_t w, const uint16_t* l43, const uint16_t* l255, uint32_t& k0, uint32_t& k1) {
+  const uint32_t wc = w ^ 0xFF00FF00u;
+  const uint32_t cr = __builtin_amdgcn_udot4(w, 102u << 24, (uint32_t)-14248, false);
+  const uint32_t cg = __builtin_amdgcn_udot4(wc, (25u << 8) | (52u << 24), (uint32_t)-10939, false);
+  const uint32_t cb = __builtin_amdgcn_udot4(w, 129u << 8, (uint32_t)-17672, false);
+  const uint32_t Y = w & 0x00FF00FFu;
+  const uint32_t R = pk_chan(Y, cr), G = pk_chan(Y, cg), B = pk_chan(Y, cb);
+  uint32_t MX, MN, D, dBR, dRG, dGB;
+  asm("v_pk_max_i16 %0, %1, %2" : "=v"(MX) : "v"(R), "v"(G));
+  asm("v_pk_max_i16 %0, %0, %1" : "+v"(MX) : "v"(B));
+  asm("v_pk_min_i16 %0, %1, %2" : "=v"(MN) : "v"(R), "v"(G));
+  asm("v_pk_min_i16 %0, %0, %1" : "+v"(MN) : "v"(B));
+  asm("v_pk_sub_u16 %0, %1, %2" : "=v"(D) : "v"(MX), "v"(MN));
+  asm("v_pk_sub_u16 %0, %1, %2" : "=v"(dBR) : "v"(B), "v"(R));
+  asm("v_pk_sub_u16 %0, %1, %2" : "=v"(dRG) : "v"(R), "v"(G));
+  asm("v_pk_sub_u16 %0, %1, %2" : "=v"(dGB) : "v"(G), "v"(B));
+  uint64_t eg0, eb0, eg1, eb1;
+  asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:WORD_0 src1_sel:WORD_0" : "=s"(eg0) : "v"(MX), "v"(G));
+  asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:WORD_0 src1_sel:WORD_0" : "=s"(eb0) : "v"(MX), "v"(B));
+  asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:WORD_1 src1_sel:WORD_1" : "=s"(eg1) : "v"(MX), "v"(G));
+  asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:WORD_1 src1_sel:WORD_1" : "=s"(eb1) : "v"(MX), "v"(B));
+  uint32_t df0, df1, b0, b1;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(df0) : "v"(dGB), "v"(dRG), "s"(eb0));
+  asm("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(df0) : "v"(dBR), "s"(eg0));
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(df1) : "v"(dGB), "v"(dRG), "s"(eb1));
+  asm("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(df1) : "v"(dBR), "s"(eg1));
+  asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(b0) : "v"(43690u), "s"(eb0));
+  asm("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(b0) : "v"(21845u), "s"(eg0));
+  asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(b1) : "v"(43690u), "s"(eb1));
+  asm("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(b1) : "v"(21845u), "s"(eg1));
+  uint32_t a43_0, a43_1, a255_0, a255_1;
+  asm("v_lshlrev_b32_sdwa %0, 1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0" : "=v"(a43_0) : "v"(D));
+  asm("v_lshlrev_b32_sdwa %0, 1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1" : "=v"(a43_1) : "v"(D));
+  asm("v_lshlrev_b32_sdwa %0, 1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0" : "=v"(a255_0) : "v"(MX));
+  asm("v_lshlrev_b32_sdwa %0, 1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1" : "=v"(a255_1) : "v"(MX));
+  const uint32_t m0 = *(const uint16_t*)((const char*)l43 + a43_0), m1 = *(const uint16_t*)((const char*)l43 + a43_1);
+  const uint32_t q0 = *(const uint16_t*)((const char*)l255 + a255_0), q1 = *(const uint16_t*)((const char*)l255 + a255_1);
+  uint32_t h0, h1, p0, p1;
+  asm("v_mad_i32_i16 %0, %1, %2, %3" : "=v"(h0) : "v"(df0), "v"(m0), "v"(b0));
+  asm("v_mad_i32_i16 %0, %1, %2, %3 op_sel:[1,0,0,0]" : "=v"(h1) : "v"(df1), "v"(m1), "v"(b1));
+  asm("v_mul_u32_u24_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0" : "=v"(p0) : "v"(q0), "v"(D));
+  asm("v_mul_u32_u24_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1" : "=v"(p1) : "v"(q1), "v"(D));
+  const uint32_t t0 = __builtin_amdgcn_perm(p0, h0, 0x0C0C0501u), t1 = __builtin_amdgcn_perm(p1, h1, 0x0C0C0501u);
+  k0 = (MX << 16) | t0;
+  k1 = (MX & 0xFFFF0000u) | t1;
+}
 template <int LAYOUT>
 __global__ __launch_bounds__(kRangeBlock) void auto_range_vec_kernel(AutoRangeArgs a, AutoVecGeom g) {
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -652,32 +700,35 @@ __global__ __launch_bounds__(kRangeBlock) void auto_range_vec_kernel(AutoRangeAr
         for (int i = 0; i < NW; ++i) {
           const int c = x0[b] + 2 * i;
           const uint32_t pos = (uint32_t)row[b] * (uint32_t)a.width + (uint32_t)c;
-          const uint32_t k0 = hsv_key<0>(w[b][i], l43, l255), k1 = hsv_key<1>(w[b][i], l43, l255);
+          uint32_t k0, k1;
+          hsv_key2(w[b][i], l43, l255, k0, k1);
           if (ok[b] && c >= g.c0 && c < g.c1) fn(k0, pos);
           if (ok[b] && c + 1 >= g.c0 && c + 1 < g.c1) fn(k1, pos + 1u);
         }
       }
     }
   };
-  // pass 1: run-length encoded counts
-  uint32_t rk = 0u, rl = 0u;
-  auto flush = [&]() {
-    if (rl) {
-      atomicAdd(&cnt[wave][0][rk & 0xFFu], rl);
-      atomicAdd(&cnt[wave][1][(rk >> 8) & 0xFFu], rl);
-      atomicAdd(&cnt[wave][2][rk >> 16], rl);
-    }
-  };
+  // pass 1: run-length encoded counts per channel
+  // (each channel on its own: a triple's run breaks whenever any channel
+  // changes -- on scene gradients nearly every pixel, on uniform bytes every
+  // one; per channel, uniform frames -32 %, scripts/ab/r06q_hsv2.py)
+  uint32_t rk3[3] = {~0u, ~0u, ~0u}, rl3[3] = {0u, 0u, 0u};
   walk([&](uint32_t key, uint32_t) {
-    if (rl && key == rk) {
-      ++rl;
-    } else {
-      flush();
-      rk = key;
-      rl = 1u;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const uint32_t v = (key >> (8 * c)) & 0xFFu;
+      if (v != rk3[c]) {
+        if (rl3[c]) atomicAdd(&cnt[wave][c][rk3[c]], rl3[c]);
+        rk3[c] = v;
+        rl3[c] = 1u;
+      } else {
+        ++rl3[c];
+      }
     }
   });
-  flush();
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+    if (rl3[c]) atomicAdd(&cnt[wave][c][rk3[c]], rl3[c]);
   __syncthreads();
   for (int i = tid; i < 3 * 256; i += kRangeBlock) {
     uint32_t n = 0;
