@@ -563,72 +563,54 @@ struct AutoVecGeom {
   uint32_t total;      // zone rows * chunks per row
 };
 
-// One of R, G, B for both pixels of a word, one per 16-bit half: Y holds Y0
-// and Y1 in its halves, c the channel's chroma term (its low 16 bits, used
-// for both halves).  (74 Y + c) mod 2^16 is the reference's 16-bit _add2 sum
-// (the B channel's wrap included), then >> 6 with the sign of bit 15 and the
-// clamp to [0, 255] (WSEQ:181-205; clamp8_shift6 per pixel).
-__device__ __forceinline__ uint32_t pk_chan(uint32_t Y, uint32_t c) {
-  uint32_t x;
-  asm("v_pk_mad_u16 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(x) : "v"(Y), "v"(74u), "v"(c));
-  asm("v_pk_ashrrev_i16 %0, 6, %0 op_sel_hi:[0,1]" : "+v"(x));
-  asm("v_pk_max_i16 %0, %0, 0" : "+v"(x));
-  asm("v_pk_min_i16 %0, %0, %1 op_sel_hi:[1,0]" : "+v"(x) : "v"(255u));
-  return x;
+// Two pixels in the 16-bit halves of one register (packed VOP3P arithmetic;
+// plain vector types and builtins, so the compiler schedules the packed ops
+// and inserts their wait states -- an inline-asm form computed wrong S values
+// under another schedule, scripts/ab/r06u_hsv3.py)
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+
+// One of R, G, B for both pixels of a word: Y holds Y0 and Y1 in its halves,
+// c the channel's chroma term (its low 16 bits, used for both).  (74 Y + c)
+// mod 2^16 is the reference's 16-bit _add2 sum (the B channel's wrap
+// included), then >> 6 with the sign of bit 15 and the clamp to [0, 255]
+// (WSEQ:181-205; clamp8_shift6 per pixel).
+__device__ __forceinline__ i16x2 pk_chan(u16x2 Y, uint32_t c) {
+  const u16x2 cc = {(unsigned short)c, (unsigned short)c};
+  const u16x2 x = Y * (u16x2){74, 74} + cc;
+  const i16x2 s = __builtin_bit_cast(i16x2, x) >> (i16x2){6, 6};
+  return __builtin_elementwise_min(__builtin_elementwise_max(s, (i16x2){0, 0}), (i16x2){255, 255});
 }
+
 // (H | S << 8 | V << 16) of both pixels of the YUYV-ordered word w (Y0 U Y1
 // V): WSEQ:207-249 for two pixels at once.  R, G, B, their max, min and the
-// three hue differences in packed 16-bit halves; the hue case selects,
-// LUT43 / LUT255 reads and products per pixel (v_mad_i32_i16 and SDWA take
-// the pixel's half).  52 VALU per word and no branches, against 66 and two
-// divergent branches per pixel for hsv_bytes' form (round 6,
-// scripts/ab/r06q_hsv2.py).
-__device__ __forceinline__ void hsv_key2(uint32_t w, const uint16_t* l43, const uint16_t* l255, uint32_t& k0, uint32_t& k1) {
+// three hue differences in packed halves; the hue case selects, LUT43 /
+// LUT255 reads and products per pixel.  ~54 VALU per word and no branches,
+// against 66 and two divergent branches per pixel for hsv_bytes' form.
+__device__ __forceinline__ void hsv_key2(uint32_t w, const uint16_t* l43, const uint16_t* l255, uint32_t& k0,
+                                         uint32_t& k1) {
   const uint32_t wc = w ^ 0xFF00FF00u;
+  // the chroma terms (Y weight 0); their low 16 bits are the wrapped sums' offsets
   const uint32_t cr = __builtin_amdgcn_udot4(w, 102u << 24, (uint32_t)-14248, false);
   const uint32_t cg = __builtin_amdgcn_udot4(wc, (25u << 8) | (52u << 24), (uint32_t)-10939, false);
   const uint32_t cb = __builtin_amdgcn_udot4(w, 129u << 8, (uint32_t)-17672, false);
-  const uint32_t Y = w & 0x00FF00FFu;
-  const uint32_t R = pk_chan(Y, cr), G = pk_chan(Y, cg), B = pk_chan(Y, cb);
-  uint32_t MX, MN, D, dBR, dRG, dGB;
-  asm("v_pk_max_i16 %0, %1, %2" : "=v"(MX) : "v"(R), "v"(G));
-  asm("v_pk_max_i16 %0, %0, %1" : "+v"(MX) : "v"(B));
-  asm("v_pk_min_i16 %0, %1, %2" : "=v"(MN) : "v"(R), "v"(G));
-  asm("v_pk_min_i16 %0, %0, %1" : "+v"(MN) : "v"(B));
-  asm("v_pk_sub_u16 %0, %1, %2" : "=v"(D) : "v"(MX), "v"(MN));
-  asm("v_pk_sub_u16 %0, %1, %2" : "=v"(dBR) : "v"(B), "v"(R));
-  asm("v_pk_sub_u16 %0, %1, %2" : "=v"(dRG) : "v"(R), "v"(G));
-  asm("v_pk_sub_u16 %0, %1, %2" : "=v"(dGB) : "v"(G), "v"(B));
-  uint64_t eg0, eb0, eg1, eb1;
-  asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:WORD_0 src1_sel:WORD_0" : "=s"(eg0) : "v"(MX), "v"(G));
-  asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:WORD_0 src1_sel:WORD_0" : "=s"(eb0) : "v"(MX), "v"(B));
-  asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:WORD_1 src1_sel:WORD_1" : "=s"(eg1) : "v"(MX), "v"(G));
-  asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:WORD_1 src1_sel:WORD_1" : "=s"(eb1) : "v"(MX), "v"(B));
-  uint32_t df0, df1, b0, b1;
-  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(df0) : "v"(dGB), "v"(dRG), "s"(eb0));
-  asm("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(df0) : "v"(dBR), "s"(eg0));
-  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(df1) : "v"(dGB), "v"(dRG), "s"(eb1));
-  asm("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(df1) : "v"(dBR), "s"(eg1));
-  asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(b0) : "v"(43690u), "s"(eb0));
-  asm("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(b0) : "v"(21845u), "s"(eg0));
-  asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(b1) : "v"(43690u), "s"(eb1));
-  asm("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(b1) : "v"(21845u), "s"(eg1));
-  uint32_t a43_0, a43_1, a255_0, a255_1;
-  asm("v_lshlrev_b32_sdwa %0, 1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0" : "=v"(a43_0) : "v"(D));
-  asm("v_lshlrev_b32_sdwa %0, 1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1" : "=v"(a43_1) : "v"(D));
-  asm("v_lshlrev_b32_sdwa %0, 1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0" : "=v"(a255_0) : "v"(MX));
-  asm("v_lshlrev_b32_sdwa %0, 1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1" : "=v"(a255_1) : "v"(MX));
-  const uint32_t m0 = *(const uint16_t*)((const char*)l43 + a43_0), m1 = *(const uint16_t*)((const char*)l43 + a43_1);
-  const uint32_t q0 = *(const uint16_t*)((const char*)l255 + a255_0), q1 = *(const uint16_t*)((const char*)l255 + a255_1);
-  uint32_t h0, h1, p0, p1;
-  asm("v_mad_i32_i16 %0, %1, %2, %3" : "=v"(h0) : "v"(df0), "v"(m0), "v"(b0));
-  asm("v_mad_i32_i16 %0, %1, %2, %3 op_sel:[1,0,0,0]" : "=v"(h1) : "v"(df1), "v"(m1), "v"(b1));
-  asm("v_mul_u32_u24_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0" : "=v"(p0) : "v"(q0), "v"(D));
-  asm("v_mul_u32_u24_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1" : "=v"(p1) : "v"(q1), "v"(D));
-  const uint32_t t0 = __builtin_amdgcn_perm(p0, h0, 0x0C0C0501u), t1 = __builtin_amdgcn_perm(p1, h1, 0x0C0C0501u);
-  k0 = (MX << 16) | t0;
-  k1 = (MX & 0xFFFF0000u) | t1;
+  const u16x2 Y = __builtin_bit_cast(u16x2, w & 0x00FF00FFu);
+  const i16x2 R = pk_chan(Y, cr), G = pk_chan(Y, cg), B = pk_chan(Y, cb);
+  const i16x2 MX = __builtin_elementwise_max(__builtin_elementwise_max(R, G), B);
+  const i16x2 MN = __builtin_elementwise_min(__builtin_elementwise_min(R, G), B);
+  const i16x2 D = MX - MN, dBR = B - R, dRG = R - G, dGB = G - B;
+  // priority G > B > R (WSEQ:226-246)
+  const bool eg0 = MX.x == G.x, eb0 = MX.x == B.x, eg1 = MX.y == G.y, eb1 = MX.y == B.y;
+  const i16x2 df0 = eg0 ? dBR : (eb0 ? dRG : dGB), df1 = eg1 ? dBR : (eb1 ? dRG : dGB);
+  const int b0 = eg0 ? 21845 : (eb0 ? 43690 : 0), b1 = eg1 ? 21845 : (eb1 ? 43690 : 0);
+  const uint32_t d0 = (uint16_t)D.x, d1 = (uint16_t)D.y, m0 = (uint16_t)MX.x, m1 = (uint16_t)MX.y;
+  const int h0 = b0 + (int)l43[d0] * (int)df0.x, h1 = b1 + (int)l43[d1] * (int)df1.y;
+  const uint32_t p0 = (uint32_t)l255[m0] * d0, p1 = (uint32_t)l255[m1] * d1;  // S = byte 1 (< 2^16)
+  // H = byte 1 of h, S = byte 1 of p, V = the maximum
+  k0 = __builtin_amdgcn_perm(p0, (uint32_t)h0, 0x0C0C0501u) | (m0 << 16);
+  k1 = __builtin_amdgcn_perm(p1, (uint32_t)h1, 0x0C0C0501u) | (m1 << 16);
 }
+
 template <int LAYOUT>
 __global__ __launch_bounds__(kRangeBlock) void auto_range_vec_kernel(AutoRangeArgs a, AutoVecGeom g) {
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
