@@ -550,7 +550,7 @@ __global__ __launch_bounds__(kBlock) void auto_range_kernel(AutoRangeArgs a) {
 //  * Pass 1 counts only: a lane run-length encodes each of H, S, V of its
 //    pixels in scan order and adds each run once to its wave's LDS
 //    histogram of that channel (one atomic per run, not per pixel); the two
-//    pixels of a word share one packed HSV computation (hsv_key2).
+//    pixels of a word share one packed HSV computation (hsv_pair).
 //  * The winner of a channel whose maximum count M is held by one value is
 //    that value.  Only channels where several values reach M need their last
 //    occurrences (see the file comment): pass 2 recomputes the zone's HSV and
@@ -582,13 +582,13 @@ __device__ __forceinline__ i16x2 pk_chan(u16x2 Y, uint32_t c) {
   return __builtin_elementwise_min(__builtin_elementwise_max(s, (i16x2){0, 0}), (i16x2){255, 255});
 }
 
-// (H | S << 8 | V << 16) of both pixels of the YUYV-ordered word w (Y0 U Y1
-// V): WSEQ:207-249 for two pixels at once.  R, G, B, their max, min and the
+// H, S, V of both pixels of the YUYV-ordered word w (Y0 U Y1 V), one value
+// per channel: WSEQ:207-249 for two pixels at once.  R, G, B, their max, min and the
 // three hue differences in packed halves; the hue case selects, LUT43 /
 // LUT255 reads and products per pixel.  ~54 VALU per word and no branches,
 // against 66 and two divergent branches per pixel for hsv_bytes' form.
-__device__ __forceinline__ void hsv_key2(uint32_t w, const uint16_t* l43, const uint16_t* l255, uint32_t& k0,
-                                         uint32_t& k1) {
+__device__ __forceinline__ void hsv_pair(uint32_t w, const uint16_t* l43, const uint16_t* l255, uint32_t (&p0)[3],
+                                         uint32_t (&p1)[3]) {
   const uint32_t wc = w ^ 0xFF00FF00u;
   // the chroma terms (Y weight 0); their low 16 bits are the wrapped sums' offsets
   const uint32_t cr = __builtin_amdgcn_udot4(w, 102u << 24, (uint32_t)-14248, false);
@@ -605,10 +605,12 @@ __device__ __forceinline__ void hsv_key2(uint32_t w, const uint16_t* l43, const 
   const int b0 = eg0 ? 21845 : (eb0 ? 43690 : 0), b1 = eg1 ? 21845 : (eb1 ? 43690 : 0);
   const uint32_t d0 = (uint16_t)D.x, d1 = (uint16_t)D.y, m0 = (uint16_t)MX.x, m1 = (uint16_t)MX.y;
   const int h0 = b0 + (int)l43[d0] * (int)df0.x, h1 = b1 + (int)l43[d1] * (int)df1.y;
-  const uint32_t p0 = (uint32_t)l255[m0] * d0, p1 = (uint32_t)l255[m1] * d1;  // S = byte 1 (< 2^16)
-  // H = byte 1 of h, S = byte 1 of p, V = the maximum
-  k0 = __builtin_amdgcn_perm(p0, (uint32_t)h0, 0x0C0C0501u) | (m0 << 16);
-  k1 = __builtin_amdgcn_perm(p1, (uint32_t)h1, 0x0C0C0501u) | (m1 << 16);
+  p0[0] = ((uint32_t)h0 >> 8) & 0xFFu;
+  p1[0] = ((uint32_t)h1 >> 8) & 0xFFu;
+  p0[1] = ((uint32_t)l255[m0] * d0) >> 8;  // (< 256)
+  p1[1] = ((uint32_t)l255[m1] * d1) >> 8;
+  p0[2] = m0;
+  p1[2] = m1;
 }
 
 template <int LAYOUT>
@@ -682,10 +684,10 @@ __global__ __launch_bounds__(kRangeBlock) void auto_range_vec_kernel(AutoRangeAr
         for (int i = 0; i < NW; ++i) {
           const int c = x0[b] + 2 * i;
           const uint32_t pos = (uint32_t)row[b] * (uint32_t)a.width + (uint32_t)c;
-          uint32_t k0, k1;
-          hsv_key2(w[b][i], l43, l255, k0, k1);
-          if (ok[b] && c >= g.c0 && c < g.c1) fn(k0, pos);
-          if (ok[b] && c + 1 >= g.c0 && c + 1 < g.c1) fn(k1, pos + 1u);
+          uint32_t h0[3], h1[3];
+          hsv_pair(w[b][i], l43, l255, h0, h1);
+          if (ok[b] && c >= g.c0 && c < g.c1) fn(h0, pos);
+          if (ok[b] && c + 1 >= g.c0 && c + 1 < g.c1) fn(h1, pos + 1u);
         }
       }
     }
@@ -695,10 +697,10 @@ __global__ __launch_bounds__(kRangeBlock) void auto_range_vec_kernel(AutoRangeAr
   // changes -- on scene gradients nearly every pixel, on uniform bytes every
   // one; per channel, uniform frames -32 %, scripts/ab/r06q_hsv2.py)
   uint32_t rk3[3] = {~0u, ~0u, ~0u}, rl3[3] = {0u, 0u, 0u};
-  walk([&](uint32_t key, uint32_t) {
+  walk([&](const uint32_t (&hv)[3], uint32_t) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      const uint32_t v = (key >> (8 * c)) & 0xFFu;
+      const uint32_t v = hv[c];
       if (v != rk3[c]) {
         if (rl3[c]) atomicAdd(&cnt[wave][c][rk3[c]], rl3[c]);
         rk3[c] = v;
@@ -731,10 +733,10 @@ __global__ __launch_bounds__(kRangeBlock) void auto_range_vec_kernel(AutoRangeAr
   __syncthreads();
   const uint32_t tie = (n_top[0] > 1u ? 1u : 0u) | (n_top[1] > 1u ? 2u : 0u) | (n_top[2] > 1u ? 4u : 0u);
   if (tie) {  // (workgroup-uniform) pass 2: the last occurrences of the tied values
-    walk([&](uint32_t key, uint32_t pos) {
+    walk([&](const uint32_t (&hv)[3], uint32_t pos) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        const uint32_t v = (key >> (8 * k)) & 0xFFu;
+        const uint32_t v = hv[k];
         if (((tie >> k) & 1u) && cnt[0][k][v] == top_n[k]) atomicMax(&lst[k][v], pos);
       }
     });
