@@ -30,10 +30,15 @@ HBM_PEAK_GBS = 8000.0
 
 def timed(fn, stream, iters):
     """Average GPU time per call of `iters` back-to-back calls (asynchronous
-    launches, so host-side call overhead overlaps the previous call's kernels)."""
+    launches, so host-side call overhead overlaps the previous call's kernels),
+    after `iters` untimed calls of the same operation (the first calls after
+    another operation's batches run up to 25 % slower: the auto-range launches
+    right after the previews' 1.9 GB of stores took 198 -> 161 us in
+    profiles/r06/r06x_operator_kernel_trace_auto_range.txt)."""
     import torch
 
-    fn()
+    for _ in range(iters):
+        fn()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record(stream)
