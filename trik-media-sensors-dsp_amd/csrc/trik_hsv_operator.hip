@@ -561,6 +561,7 @@ struct AutoVecGeom {
   int32_t k0;          // first chunk column
   FastDiv per_row;     // chunks per zone row
   uint32_t total;      // zone rows * chunks per row
+  int32_t lo_f, hi_l;  // a row's first chunk: pixels p < lo_f lie left of the zone; its last: p >= hi_l right of it
 };
 
 // Two pixels in the 16-bit halves of one register (packed VOP3P arithmetic;
@@ -695,24 +696,58 @@ __global__ __launch_bounds__(kRangeBlock) void auto_range_vec_kernel(AutoRangeAr
   // pass 1: run-length encoded counts per channel
   // (each channel on its own: a triple's run breaks whenever any channel
   // changes -- on scene gradients nearly every pixel, on uniform bytes every
-  // one; per channel, uniform frames -32 %, scripts/ab/r06q_hsv2.py)
-  uint32_t rk3[3] = {~0u, ~0u, ~0u}, rl3[3] = {0u, 0u, 0u};
-  walk([&](const uint32_t (&hv)[3], uint32_t) {
+  // one; per channel, uniform frames -32 %, scripts/ab/r06q_hsv2.py).  Every
+  // pixel of a chunk is counted; the few outside the zone's columns (a row's
+  // first chunk p < lo_f, its last p >= hi_l: kernel-wide constants) are
+  // subtracted again, so no pixel carries a column test (-7 %,
+  // scripts/ab/r06ab_range_attr.py).  A run's length is added when the next
+  // run starts (the first add of each channel adds 0 to bin 0).
+  uint32_t rk3[3] = {0u, 0u, 0u}, rl3[3] = {0u, 0u, 0u};
+  auto count = [&](const uint32_t (&hv)[3]) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const uint32_t v = hv[c];
-      if (v != rk3[c]) {
-        if (rl3[c]) atomicAdd(&cnt[wave][c][rk3[c]], rl3[c]);
-        rk3[c] = v;
-        rl3[c] = 1u;
-      } else {
-        ++rl3[c];
+      const bool brk = v != rk3[c];
+      if (brk) atomicAdd(&cnt[wave][c][rk3[c]], rl3[c]);
+      rl3[c] = brk ? 1u : rl3[c] + 1u;
+      rk3[c] = v;
+    }
+  };
+  auto uncount = [&](uint64_t m, const uint32_t (&hv)[3]) {  // lanes of m: this pixel lies outside the zone
+    if (m == 0) return;
+    if (__builtin_amdgcn_inverse_ballot_w64(m)) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) atomicSub(&cnt[wave][c][hv[c]], 1u);
+    }
+  };
+  const uint32_t kc_last = (uint32_t)(g.k0 + (int)g.per_row.d - 1);
+  for (uint32_t j0 = (uint32_t)tid; j0 < g.total; j0 += kVecBatch * kRangeBlock) {
+    uint32_t w[kVecBatch][NW];
+    int row[kVecBatch], x0[kVecBatch];
+    bool ok[kVecBatch];
+    load_batch(j0, w, row, x0, ok);
+#pragma unroll
+    for (int b = 0; b < kVecBatch; ++b) {
+      const uint64_t okm = __builtin_amdgcn_ballot_w64(ok[b]);
+      if (okm == 0ull) continue;
+      const uint32_t kc = (uint32_t)x0[b] / (uint32_t)(2 * NW);
+      const uint64_t firstm = __builtin_amdgcn_ballot_w64(ok[b] && kc == (uint32_t)g.k0);
+      const uint64_t lastm = __builtin_amdgcn_ballot_w64(ok[b] && kc == kc_last);
+      if (ok[b]) {
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+          uint32_t h0[3], h1[3];
+          hsv_pair(w[b][i], l43, l255, h0, h1);
+          count(h0);
+          count(h1);
+          uncount((2 * i < g.lo_f ? firstm : 0ull) | (2 * i >= g.hi_l ? lastm : 0ull), h0);
+          uncount((2 * i + 1 < g.lo_f ? firstm : 0ull) | (2 * i + 1 >= g.hi_l ? lastm : 0ull), h1);
+        }
       }
     }
-  });
+  }
 #pragma unroll
-  for (int c = 0; c < 3; ++c)
-    if (rl3[c]) atomicAdd(&cnt[wave][c][rk3[c]], rl3[c]);
+  for (int c = 0; c < 3; ++c) atomicAdd(&cnt[wave][c][rk3[c]], rl3[c]);
   __syncthreads();
   for (int i = tid; i < 3 * 256; i += kRangeBlock) {
     uint32_t n = 0;
@@ -933,6 +968,8 @@ int launch_auto_range(const AutoRangeArgs& a, hipStream_t s) {
     if ((int64_t)16 * (g.k0 + cpr) <= a.line_length) {
       g.per_row = make_div((uint32_t)(cpr > 0 ? cpr : 1));
       g.total = (uint32_t)(cpr > 0 ? (int64_t)cpr * zh : 0);
+      g.lo_f = g.c0 - g.k0 * pxc;                  // (0 .. pxc - 1)
+      g.hi_l = g.c1 - (g.k0 + (cpr > 0 ? cpr : 1) - 1) * pxc;  // (1 .. pxc)
       if (yuyv)
         hipLaunchKernelGGL(auto_range_vec_kernel<TRIK_HSV_LAYOUT_YUYV>, dim3((unsigned)a.n_frames), dim3(kRangeBlock), 0,
                            s, a, g);
