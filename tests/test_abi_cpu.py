@@ -52,6 +52,14 @@ def test_version_without_gpu(abi):
     assert abi.load().trik_hsv_last_error() == b""
 
 
+def test_set_reserved_cus_rejects_without_gpu(abi):
+    """trik_hsv_set_reserved_cus validates before touching a handle: a NULL
+    handle or a count outside 0..32 returns -1 (no GPU needed)."""
+    lib = abi.load()
+    for n in (0, 2, 32, -1, 33):
+        assert lib.trik_hsv_set_reserved_cus(None, n) == -1
+
+
 STRUCTS = ["TRIK_VIDTRANSCODE_CV_Params", "TRIK_VIDTRANSCODE_CV_DynamicParams",
            "TRIK_VIDTRANSCODE_CV_InArgsAlg", "TRIK_VIDTRANSCODE_CV_InArgs",
            "TRIK_VIDTRANSCODE_CV_OutArgsAlg", "TRIK_VIDTRANSCODE_CV_OutArgs",

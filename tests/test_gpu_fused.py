@@ -143,3 +143,31 @@ def test_fused_step_two_streams(torch_dev, hsv):
     for got in outs:
         for g, w, name in zip(got, want, ("sums", "targets", "totals")):
             assert torch.equal(g, w), name
+
+
+@pytest.mark.parametrize("n,reserve", [(1024, 2), (1100, 32), (40, 5)])
+def test_fused_step_with_reserved_cus(torch_dev, hsv, n, reserve):
+    """trik_hsv_set_reserved_cus (bench.py's --reserve-cus at N > 1): the hot
+    grid is sized to leave CUs free for another stream's kernels, so each
+    workgroup takes a larger share of the units; the fused step and the
+    separate-kernel path give the same outputs as with every CU, and the call
+    returns the previous setting and rejects values outside 0..32."""
+    torch = torch_dev
+    frames = _frames(torch, hsv, n, 0)
+    want = _separate(torch, hsv, frames, n, BENCH_RANGES)
+    det = hsv.Detector(hot=hsv.HOT_CHROMA)
+    assert det.set_reserved_cus(reserve) == 0
+    for _ in range(2):
+        got = _fused(torch, hsv, det, frames, n, BENCH_RANGES)
+        for g, w, name in zip(got, want, ("sums", "targets", "totals")):
+            assert torch.equal(g, w), (name, n, reserve)
+    sums = torch.zeros((n, 4, 3), dtype=torch.int64, device="cuda")
+    det.batch_sums(frames, W, H, LL, LAYOUT_YUYV, BENCH_RANGES, sums, n_frames=n, frame_stride=H * LL)
+    torch.cuda.synchronize()
+    assert torch.equal(sums, want[0])
+    assert det.last_hot_kernel() == hsv.HOT_CHROMA
+    for bad in (-1, 33):
+        with pytest.raises(ValueError):
+            det.set_reserved_cus(bad)
+    assert det.set_reserved_cus(0) == reserve
+    det.close()
